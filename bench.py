@@ -1,0 +1,312 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident batched page checksum throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s of device-resident batched page XXH3-64 over
+4 KiB pages on 1/2/4/8 MI355X.  A "step" is one pass of the hot path
+(pcs_pages_digest_dev -> the XXH3 page kernel) over one batch of synthetic
+pages already resident in HBM; value = page bytes hashed by ALL ranks per
+second (GiB/s, 2^30), per-GPU work fixed (weak scaling: every rank owns its
+own disjoint page range, no collective on the data path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+
+Default (N=1) = BASELINE config 2: 1,048,576 x 4 KiB pages (4 GiB) per GPU.
+Multi-GPU: launched by torch.distributed.run, one process per GPU; gloo is the
+control plane (barrier + max over ranks of the timed region).
+
+Also reported, on the same line:
+  roofline      dominant kernel's algorithmic bytes per launch / average launch
+                time (HIP events on the launch stream) vs 8 TB/s HBM peak;
+                traffic = PMC-measured HBM bytes per launch when a matching
+                rocprofv3 summary is committed under profiles/ (else null).
+  read_ceiling  the same load pattern with the hash removed (achievable rate).
+  cpu_baseline  the reference's own xxHash (oracle/_ref, one XXH3_64bits call
+                per page like page.cpp:18-31) on ONE host core over a bounded
+                sample of the same pages; its digests double as a parity check.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import eloqstore_amd as pcs  # noqa: E402
+
+METRIC = "GiB/s device-resident batched page XXH3-64, 4 KiB pages, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec 8.0 TB/s (MI355X_MICROARCH.md chip table)
+GIB = float(1 << 30)
+
+CONFIGS = {
+    # name: (page_size or None for mixed, pages per GPU, seed, description)
+    2: (4096, 1 << 20, 0x5EED0002, "config2: 4 KiB pages, 1M-page device-resident batch per GPU"),
+    3: (None, 1 << 20, 0x5EED0003, "config3: mixed 4/8/16 KiB pages, 1M pages per GPU, packed + descriptors"),
+    4: (65536, 1 << 18, 0x5EED0004, "config4: 64 KiB chunks, 256K chunks device-resident per GPU"),
+    5: (4096, 1 << 23, 0x5EED0005, "config5: 4 KiB pages, 8M pages per GPU (64M over 8 GPUs)"),
+}
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def init_dist(world: int):
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        return dist
+    return None
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+class Workload:
+    """Device-resident pages of this rank's shard plus the timed step."""
+
+    def __init__(self, cfg: int, algo: int, rank: int, pages_per_gpu: int | None, dev: str):
+        P, n, seed, desc = CONFIGS[cfg]
+        self.cfg, self.algo, self.seed, self.desc = cfg, algo, seed, desc
+        self.n = pages_per_gpu or n
+        self.first = rank * self.n  # disjoint global page range of this rank
+        self.P = P
+        self.dev = dev
+        if P is not None:
+            self.bytes = self.n * P
+            self.pages = torch.empty(self.bytes, dtype=torch.uint8, device=dev)
+            pcs.gen_pages(self.pages, P, self.n, seed, self.first)
+            self.out = torch.empty(self.n, dtype=torch.int64, device=dev)
+        else:
+            from workload import mixed_layout
+            offs, lens, total = mixed_layout(seed, self.first, self.n)
+            self.offs, self.lens = offs, lens
+            self.bytes = total
+            self.pages = torch.empty(total, dtype=torch.uint8, device=dev)
+            self.d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+            self.d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+            pcs.gen_desc(self.pages, self.d_off, self.d_len, self.n, seed, self.first)
+            self.out = torch.empty(self.n, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+
+    def step(self):
+        if self.P is not None:
+            pcs.pages_digest(self.pages, self.P, self.n, self.algo, out=self.out)
+        else:
+            pcs.desc_digest(self.pages, self.d_off, self.d_len, self.n, self.algo, out=self.out)
+
+    def algorithmic_bytes(self) -> int:
+        # every page byte read once (the 8-byte header shares the first line) + 8 B digest written
+        return self.bytes + 8 * self.n
+
+    def read_ceiling(self, reps: int) -> float | None:
+        if self.P is None or self.P not in (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
+            return None
+        pcs.read_ceiling(self.pages, self.P, self.n, self.out)
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(reps):
+            pcs.read_ceiling(self.pages, self.P, self.n, self.out)
+        ev[1].record()
+        torch.cuda.synchronize()
+        t = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+        return self.algorithmic_bytes() / t / 1e9
+
+    def sample_pages_host(self, max_bytes: int):
+        """(host uint8 array, page size, gpu digests) for a leading sample of the batch."""
+        if self.P is not None:
+            k = max(1, min(self.n, max_bytes // self.P))
+            host = self.pages[: k * self.P].cpu().numpy()
+            return host, self.P, self.out[:k].cpu().numpy().view(np.uint64)
+        return None
+
+
+def cpu_baseline(w: Workload, target_s: float):
+    """Reference xxHash on one host core over a bounded sample of the same pages."""
+    import oracle  # test/baseline infrastructure only (see oracle/__init__.py)
+
+    if w.P is None:
+        from workload import fill_desc
+        k = 4096
+        host = fill_desc(w.seed, w.first, w.offs[:k], w.lens[:k], int(w.offs[k - 1]) + int(w.lens[k - 1]))
+        gpu = w.out[:k].cpu().numpy().view(np.uint64)
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            want = oracle.desc_digest(host, w.offs[:k], w.lens[:k], w.algo)
+            reps += 1
+            if time.perf_counter() - t0 >= target_s:
+                break
+        dt = time.perf_counter() - t0
+        return {"value": reps * host.nbytes / dt / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"{k} mixed pages ({host.nbytes / 2**20:.0f} MiB) x {reps} passes, oracle restatement"}, \
+            {"pages": k, "mismatches": int((want != gpu).sum())}
+    host, P, gpu = w.sample_pages_host(256 << 20)
+    fn = oracle.ref_pages_digest if oracle.ref_lib() is not None else None
+    kind = "reference" if fn else "port"
+    if fn is None:
+        fn = oracle.pages_digest
+    want = fn(host, P, w.algo)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        fn(host, P, w.algo)
+        reps += 1
+        if time.perf_counter() - t0 >= target_s:
+            break
+    dt = time.perf_counter() - t0
+    what = ("reference external/xxhash.c v0.8.3 (gcc -O2, SSE2 path), one XXH3_64bits call per page"
+            if kind == "reference" else "oracle C restatement, one call per page")
+    if w.algo == pcs.XXH64:
+        what = what.replace("XXH3_64bits", "XXH64")
+    return {"value": reps * host.nbytes / dt / GIB, "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"first {host.nbytes // P} pages ({host.nbytes >> 20} MiB) of the batch x {reps} passes; {what}"}, \
+        {"pages": int(host.nbytes // P), "mismatches": int((want != gpu).sum())}
+
+
+def committed_traffic(cfg: int, algo: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        key = f"config{cfg}_{'xxh3' if algo == 0 else 'xxh64'}"
+        if key in d.get("traffic_bytes_per_launch", {}):
+            best = (d["traffic_bytes_per_launch"][key], os.path.relpath(path, ROOT))
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--algo", choices=["xxh3", "xxh64"], default="xxh3")
+    ap.add_argument("--pages-per-gpu", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    dist = init_dist(world)
+    torch.cuda.set_device(local)
+    pcs.lib()
+    if pcs.lib().pcs_set_device(local) != 0:
+        raise pcs.PcsError("pcs_set_device", -2, pcs.lib().pcs_last_error().decode())
+    dev = f"cuda:{local}"
+    algo = pcs.XXH3_64 if args.algo == "xxh3" else pcs.XXH64
+
+    w = Workload(args.config, algo, rank, args.pages_per_gpu, dev)
+
+    for _ in range(args.warmup):
+        w.step()
+    torch.cuda.synchronize()
+
+    # per-launch HIP events on the launch stream (torch's current stream)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier(dist)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record()
+        w.step()
+        ends[i].record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t1 - t0)
+    launch_s = sorted(s.elapsed_time(e) / 1e3 for s, e in zip(starts, ends))
+    avg_launch = sum(launch_s) / len(launch_s)
+    total_bytes = sum_over_ranks(dist, float(w.bytes)) * args.steps
+    value = total_bytes / elapsed / GIB
+
+    ceiling = w.read_ceiling(max(3, args.steps // 5))
+    cpu, parity = (None, None)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline(w, args.cpu_seconds)
+
+    if rank == 0:
+        achieved = w.algorithmic_bytes() / avg_launch / 1e9
+        traffic = committed_traffic(args.config, algo)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: splitmix64 page words generated on device (pcs_gen_pages_dev)",
+            "config": {
+                "workload": w.desc,
+                "page_size": w.P if w.P is not None else "4/8/16 KiB mixed",
+                "pages_per_gpu": w.n,
+                "bytes_per_gpu": w.bytes,
+                "algo": "xxh3_64" if algo == 0 else "xxh64",
+                "mode": "digest (pcs_pages_digest_dev)" if w.P else "digest (pcs_desc_digest_dev)",
+                "parallelism": f"page shards x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic[0] if traffic else None,
+                "traffic_source": traffic[1] if traffic else None,
+                "algorithmic_bytes_per_launch": w.algorithmic_bytes(),
+                "avg_launch_ms": round(avg_launch * 1e3, 4),
+                "min_launch_ms": round(launch_s[0] * 1e3, 4),
+            },
+            "read_ceiling_GBps": round(ceiling, 1) if ceiling else None,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,254 @@
+"""eloqstore_amd — Python binding of the MI355X page-checksum engine.
+
+The product is the native library ``libeloqstore_pcs.so`` (HIP kernels for
+gfx950 + C ABI declared in ``include/eloqstore_pcs.h`` + the C++ drop-in
+``include/eloqstore/page_checksum.h``).  This module is the thin ctypes layer
+the tests and ``bench.py`` drive it through; device memory and streams come
+from PyTorch (plumbing only).  There is no CPU fallback: every compute call
+raises ``PcsError`` when the library or the GPU is unavailable.
+
+Mirrors the reference call surface (src/storage/page.cpp:18-31):
+``set_checksum`` / ``validate_checksum`` on one host page, plus batched
+device and host forms.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (loads the process's HIP runtime before the library)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libeloqstore_pcs.so")
+TOOL_PATH = os.path.join(HERE, "page_checksum_tool")
+HEADER_PATH = os.path.join(ROOT, "include", "eloqstore_pcs.h")
+
+XXH3_64 = 0
+XXH64 = 1
+PCS_OK = 0
+PCS_ERR_INVALID = -1
+PCS_ERR_NO_DEVICE = -2
+PCS_ERR_HIP = -3
+PCS_ERR_NOMEM = -4
+
+_u64, _u32, _i32, _vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+_P = ctypes.POINTER
+
+# name -> argtypes (restype int unless listed in _STR)
+_SIGS = {
+    "pcs_device_count": [_P(_i32)],
+    "pcs_set_device": [_i32],
+    "pcs_synchronize": [_vp],
+    "pcs_pages_digest_dev": [_vp, _u64, _u64, _i32, _vp, _vp],
+    "pcs_pages_validate_dev": [_vp, _u64, _u64, _i32, _vp, _vp, _vp],
+    "pcs_pages_stamp_dev": [_vp, _u64, _u64, _i32, _vp],
+    "pcs_desc_digest_dev": [_vp, _vp, _vp, _u64, _i32, _vp, _vp],
+    "pcs_desc_validate_dev": [_vp, _vp, _vp, _u64, _i32, _vp, _vp, _vp],
+    "pcs_desc_stamp_dev": [_vp, _vp, _vp, _u64, _i32, _vp],
+    "pcs_xxh3_64_ranges_dev": [_vp, _vp, _vp, _u64, _vp, _vp],
+    "pcs_xxh64_ranges_dev": [_vp, _vp, _vp, _u64, _u64, _vp, _vp],
+    "pcs_pages_validate_host": [_vp, _u64, _u64, _i32, _vp, _vp],
+    "pcs_pages_stamp_host": [_vp, _u64, _u64, _i32],
+    "pcs_pages_digest_host": [_vp, _u64, _u64, _i32, _vp],
+    "pcs_shard_range": [_u64, _i32, _i32, _P(_u64), _P(_u64)],
+    "pcs_gen_pages_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
+    "pcs_gen_desc_dev": [_vp, _vp, _vp, _u64, _u64, _u64, _vp],
+    "pcs_flip_byte_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
+    "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
+    "pcs_version": [],
+    "pcs_last_error": [],
+}
+_STR = {"pcs_version", "pcs_last_error"}
+
+
+class PcsError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libeloqstore_pcs.so (built by __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PcsError("load", PCS_ERR_NO_DEVICE,
+                           f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        so = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            f = getattr(so, name)
+            f.argtypes = args
+            f.restype = ctypes.c_char_p if name in _STR else ctypes.c_int
+        _lib = so
+    return _lib
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Every pcs_* function declared in the public C header."""
+    with open(path) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(pcs_[a-z0-9_]+)\s*\(", text)))
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != PCS_OK:
+        raise PcsError(fn, rc, lib().pcs_last_error().decode(errors="replace"))
+
+
+def _call(fn: str, *args) -> None:
+    _check(fn, getattr(lib(), fn)(*args))
+
+
+def _ptr(t) -> int:
+    if t is None:
+        return 0
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def version() -> str:
+    return lib().pcs_version().decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().pcs_device_count(ctypes.byref(n))
+    return n.value if rc == PCS_OK else 0
+
+
+def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
+    b, e = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _call("pcs_shard_range", n, world, rank, ctypes.byref(b), ctypes.byref(e))
+    return b.value, e.value
+
+
+# ---- device-resident batches (torch tensors on cuda) ------------------------
+
+def pages_digest(pages, page_size: int, n: int, algo: int = XXH3_64, out=None, stream=None):
+    """digests[i] = hash of page i over [8, page_size); pages: uint8 device tensor."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=pages.device)
+    _call("pcs_pages_digest_dev", _ptr(pages), page_size, n, algo, _ptr(out), _stream(stream))
+    return out
+
+
+def pages_validate(pages, page_size: int, n: int, algo: int = XXH3_64, ok=None, first_bad=None, stream=None):
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=pages.device)
+    if first_bad is None:
+        first_bad = torch.empty(1, dtype=torch.int64, device=pages.device)
+    _call("pcs_pages_validate_dev", _ptr(pages), page_size, n, algo, _ptr(ok), _ptr(first_bad), _stream(stream))
+    return ok, first_bad
+
+
+def pages_stamp(pages, page_size: int, n: int, algo: int = XXH3_64, stream=None) -> None:
+    _call("pcs_pages_stamp_dev", _ptr(pages), page_size, n, algo, _stream(stream))
+
+
+def desc_digest(base, off, length, n: int, algo: int = XXH3_64, out=None, stream=None):
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=base.device)
+    _call("pcs_desc_digest_dev", _ptr(base), _ptr(off), _ptr(length), n, algo, _ptr(out), _stream(stream))
+    return out
+
+
+def desc_validate(base, off, length, n: int, algo: int = XXH3_64, ok=None, first_bad=None, stream=None):
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=base.device)
+    if first_bad is None:
+        first_bad = torch.empty(1, dtype=torch.int64, device=base.device)
+    _call("pcs_desc_validate_dev", _ptr(base), _ptr(off), _ptr(length), n, algo, _ptr(ok), _ptr(first_bad),
+          _stream(stream))
+    return ok, first_bad
+
+
+def desc_stamp(base, off, length, n: int, algo: int = XXH3_64, stream=None) -> None:
+    _call("pcs_desc_stamp_dev", _ptr(base), _ptr(off), _ptr(length), n, algo, _stream(stream))
+
+
+def xxh3_64_ranges(base, off, length, n: int, out=None, stream=None):
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=base.device)
+    _call("pcs_xxh3_64_ranges_dev", _ptr(base), _ptr(off), _ptr(length), n, _ptr(out), _stream(stream))
+    return out
+
+
+def xxh64_ranges(base, off, length, n: int, seed: int = 0, out=None, stream=None):
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=base.device)
+    _call("pcs_xxh64_ranges_dev", _ptr(base), _ptr(off), _ptr(length), n, seed, _ptr(out), _stream(stream))
+    return out
+
+
+def gen_pages(pages, page_size: int, n: int, seed: int, first_page: int = 0, stream=None) -> None:
+    _call("pcs_gen_pages_dev", _ptr(pages), page_size, n, seed, first_page, _stream(stream))
+
+
+def gen_desc(base, off, length, n: int, seed: int, first_page: int = 0, stream=None) -> None:
+    _call("pcs_gen_desc_dev", _ptr(base), _ptr(off), _ptr(length), n, seed, first_page, _stream(stream))
+
+
+def flip_byte(pages, page_size: int, n: int, every: int, byte_offset: int = 10, stream=None) -> None:
+    _call("pcs_flip_byte_dev", _ptr(pages), page_size, n, every, byte_offset, _stream(stream))
+
+
+def read_ceiling(pages, page_size: int, n: int, out, stream=None) -> None:
+    _call("pcs_read_ceiling_dev", _ptr(pages), page_size, n, _ptr(out), _stream(stream))
+
+
+# ---- host-memory forms (reference call surface) ------------------------------
+
+def _page_ptrs(pages: list) -> tuple:
+    bufs = [p if isinstance(p, ctypes.Array) else (ctypes.c_char * len(p)).from_buffer(p) for p in pages]
+    arr = (ctypes.c_void_p * len(bufs))(*[ctypes.addressof(b) for b in bufs])
+    return arr, bufs
+
+
+def set_checksum(page: bytearray) -> None:
+    """eloqstore::SetChecksum (page.cpp:18-23) on one writable host page."""
+    arr, _keep = _page_ptrs([page])
+    _call("pcs_pages_stamp_host", arr, len(page), 1, XXH3_64)
+
+
+def validate_checksum(page) -> bool:
+    """eloqstore::ValidateChecksum (page.cpp:25-31) on one host page."""
+    buf = page if isinstance(page, bytearray) else bytearray(page)
+    arr, _keep = _page_ptrs([buf])
+    ok = (ctypes.c_uint8 * 1)()
+    _call("pcs_pages_validate_host", arr, len(buf), 1, XXH3_64, ok, None)
+    return bool(ok[0])
+
+
+def validate_checksums(pages: list, page_size: int, algo: int = XXH3_64):
+    """Batched ValidateChecksum over scattered host pages -> (ok list, first_bad or None)."""
+    arr, _keep = _page_ptrs(pages)
+    ok = (ctypes.c_uint8 * len(pages))()
+    fb = ctypes.c_uint64(0)
+    _call("pcs_pages_validate_host", arr, page_size, len(pages), algo, ok, ctypes.byref(fb))
+    return list(ok), (None if fb.value == (1 << 64) - 1 else fb.value)
+
+
+def set_checksums(pages: list, page_size: int, algo: int = XXH3_64) -> None:
+    arr, _keep = _page_ptrs(pages)
+    _call("pcs_pages_stamp_host", arr, page_size, len(pages), algo)
+
+
+def page_digests_host(pages: list, page_size: int, algo: int = XXH3_64) -> list:
+    arr, _keep = _page_ptrs(pages)
+    out = (ctypes.c_uint64 * len(pages))()
+    _call("pcs_pages_digest_host", arr, page_size, len(pages), algo, out)
+    return list(out)

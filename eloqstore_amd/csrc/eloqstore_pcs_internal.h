@@ -1,0 +1,31 @@
+// eloqstore_pcs_internal.h — launch entry points shared by the C ABI
+// (pcs_capi.cpp) and the kernels (pcs_kernels.hip).  Not installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pcs {
+
+// mode: 0 digest, 1 validate, 2 stamp.  algo: 0 XXH3-64, 1 XXH64.
+// Fixed-stride pages; returns hipErrorNotSupported when the shape needs the
+// descriptor path (unaligned base, odd page size).
+hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t* out,
+                     uint8_t* ok, unsigned long long* first_bad, hipStream_t s);
+
+// Descriptor batch: range i = [base + off[i], +len[i]).  skip = 8 applies the
+// page convention (digest over [8, len), stored digest at [0, 8)); skip = 0
+// hashes the raw range.  seed is used by XXH64 only (XXH3 path is seed 0).
+hipError_t run_desc(int mode, int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
+                    int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* first_bad,
+                    hipStream_t s);
+
+hipError_t run_gen_pages(uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t seed, uint64_t first_page,
+                         hipStream_t s);
+hipError_t run_gen_desc(uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n, uint64_t seed,
+                        uint64_t first_page, hipStream_t s);
+hipError_t run_flip(uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t every, uint64_t byte_off,
+                    hipStream_t s);
+hipError_t run_read_ceiling(const uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t* out, hipStream_t s);
+
+}  // namespace pcs

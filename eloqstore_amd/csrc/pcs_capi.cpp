@@ -1,0 +1,382 @@
+// pcs_capi.cpp — extern "C" boundary of libeloqstore_pcs.so (include/eloqstore_pcs.h).
+//
+// Argument checking, error reporting and the host-memory batch pipeline
+// (gather scattered pool pages into pinned staging -> H2D -> kernel -> D2H of
+// 8-byte digests / 1-byte verdicts), double-buffered over two HIP streams.
+// All compute is on the GPU; there is no CPU hashing in this library.
+#include "eloqstore_pcs.h"
+#include "eloqstore_pcs_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int code, const std::string& msg) {
+    t_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(PCS_ERR_HIP, std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")");
+}
+
+// A compute entry point must see a usable device; otherwise fail loudly
+// (there is no CPU fallback by design).
+int require_device() {
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return fail(PCS_ERR_NO_DEVICE, std::string("no usable HIP device: ") +
+                                           (e != hipSuccess ? hipGetErrorString(e) : "device count is 0"));
+    return PCS_OK;
+}
+
+bool valid_algo(int algo) { return algo == PCS_XXH3_64 || algo == PCS_XXH64; }
+
+int finish(hipError_t e, const char* what) { return e == hipSuccess ? PCS_OK : hip_fail(e, what); }
+
+// Fixed-stride pages: fast kernels when the shape allows, else descriptor
+// path over a device-side descriptor array built on the fly.
+int pages_common(int mode, const void* d_pages, uint64_t P, uint64_t n, int algo, uint64_t* d_out, uint8_t* d_ok,
+                 uint64_t* d_first_bad, pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
+    if (P < 8) return fail(PCS_ERR_INVALID, "page_size must be >= 8 (8-byte digest header)");
+    if (P > 0xFFFFFFFFull) return fail(PCS_ERR_INVALID, "page_size must fit in 32 bits");
+    if (n && !d_pages) return fail(PCS_ERR_INVALID, "d_pages is null");
+    if (mode == 0 && n && !d_out) return fail(PCS_ERR_INVALID, "d_digests is null");
+    if (mode == 1 && n && !d_ok) return fail(PCS_ERR_INVALID, "d_ok is null");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (d_first_bad) {
+        hipError_t e = hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(first_bad)");
+    }
+    if (n == 0) return PCS_OK;
+    auto* fb = reinterpret_cast<unsigned long long*>(d_first_bad);
+    hipError_t e = pcs::run_pages(mode, algo, static_cast<const uint8_t*>(d_pages), P, n, d_out, d_ok, fb, s);
+    if (e != hipErrorNotSupported) return finish(e, "page kernel launch");
+    (void)hipGetLastError();
+    // Odd shape: descriptors (off = i*P, len = P) in a temporary device array.
+    uint64_t* d_off = nullptr;
+    uint32_t* d_len = nullptr;
+    if ((e = hipMallocAsync(reinterpret_cast<void**>(&d_off), n * 8, s)) != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    if ((e = hipMallocAsync(reinterpret_cast<void**>(&d_len), n * 4, s)) != hipSuccess) {
+        (void)hipFreeAsync(d_off, s);
+        return hip_fail(e, "hipMallocAsync");
+    }
+    std::vector<uint64_t> off(n);
+    std::vector<uint32_t> len(n, (uint32_t)P);
+    for (uint64_t i = 0; i < n; ++i) off[i] = i * P;
+    e = hipMemcpyAsync(d_off, off.data(), n * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_len, len.data(), n * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = pcs::run_desc(mode, algo, static_cast<const uint8_t*>(d_pages), d_off, d_len, n, 8, 0, d_out, d_ok, fb, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // host vectors must outlive the copies
+    (void)hipFreeAsync(d_off, s);
+    (void)hipFreeAsync(d_len, s);
+    return finish(e, "descriptor fallback");
+}
+
+int desc_common(int mode, const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, int algo,
+                int skip, uint64_t seed, uint64_t* d_out, uint8_t* d_ok, uint64_t* d_first_bad, pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
+    if (n && (!d_base || !d_off || !d_len)) return fail(PCS_ERR_INVALID, "null descriptor pointer");
+    if (mode == 0 && n && !d_out) return fail(PCS_ERR_INVALID, "d_digests is null");
+    if (mode == 1 && n && !d_ok) return fail(PCS_ERR_INVALID, "d_ok is null");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (d_first_bad) {
+        hipError_t e = hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(first_bad)");
+    }
+    if (n == 0) return PCS_OK;
+    return finish(pcs::run_desc(mode, algo, static_cast<const uint8_t*>(d_base), d_off, d_len, n, skip, seed, d_out,
+                                d_ok, reinterpret_cast<unsigned long long*>(d_first_bad), s),
+                  "descriptor kernel launch");
+}
+
+// ---------------------------------------------------------------------------
+// host-memory pipeline
+// ---------------------------------------------------------------------------
+constexpr size_t kStageBytes = 32u << 20;  // per slot
+
+struct Slot {
+    hipStream_t stream = nullptr;
+    uint8_t* h_pages = nullptr;  // pinned
+    uint8_t* d_pages = nullptr;
+    uint64_t* h_dig = nullptr;   // pinned
+    uint64_t* d_dig = nullptr;
+    uint8_t* h_ok = nullptr;     // pinned
+    uint8_t* d_ok = nullptr;
+    size_t cap_pages_bytes = 0, cap_n = 0;
+    uint64_t first = 0, count = 0;  // chunk currently in flight
+    bool busy = false;
+};
+
+struct HostCtx {
+    Slot slot[2];
+    ~HostCtx() {
+        for (auto& s : slot) {
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+            (void)hipHostFree(s.h_pages);
+            (void)hipFree(s.d_pages);
+            (void)hipHostFree(s.h_dig);
+            (void)hipFree(s.d_dig);
+            (void)hipHostFree(s.h_ok);
+            (void)hipFree(s.d_ok);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+        }
+    }
+};
+
+thread_local std::unordered_map<int, HostCtx> t_ctx;
+
+int ensure_slot(Slot& s, size_t page_bytes, size_t n) {
+    hipError_t e;
+    if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(e, "hipStreamCreate");
+    if (page_bytes > s.cap_pages_bytes) {
+        (void)hipHostFree(s.h_pages);
+        (void)hipFree(s.d_pages);
+        s.h_pages = nullptr;
+        s.d_pages = nullptr;
+        s.cap_pages_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_pages), page_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.d_pages), page_bytes) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "staging allocation failed");
+        s.cap_pages_bytes = page_bytes;
+    }
+    if (n > s.cap_n) {
+        (void)hipHostFree(s.h_dig);
+        (void)hipFree(s.d_dig);
+        (void)hipHostFree(s.h_ok);
+        (void)hipFree(s.d_ok);
+        s.h_dig = nullptr; s.d_dig = nullptr; s.h_ok = nullptr; s.d_ok = nullptr;
+        s.cap_n = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.d_dig), n * 8) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&s.h_ok), n, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.d_ok), n) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "result staging allocation failed");
+        s.cap_n = n;
+    }
+    return PCS_OK;
+}
+
+// mode 0: digests -> out_dig;  mode 1: verdicts -> out_ok (+ first_bad);
+// mode 2: digests stamped into the caller's pages.
+int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* out_ok,
+               uint64_t* first_bad, uint64_t* out_dig) {
+    if (int rc = require_device()) return rc;
+    if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
+    if (P < 8 || P > 0xFFFFFFFFull) return fail(PCS_ERR_INVALID, "page_size must be in [8, 2^32)");
+    if (n && !pages) return fail(PCS_ERR_INVALID, "pages is null");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!pages[i]) return fail(PCS_ERR_INVALID, "null page pointer in batch");
+    if (first_bad) *first_bad = UINT64_MAX;
+    if (n == 0) return PCS_OK;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    HostCtx& ctx = t_ctx[dev];
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, kStageBytes / P));
+    for (auto& s : ctx.slot)
+        if (int rc = ensure_slot(s, chunk * P, chunk)) return rc;
+
+    uint64_t bad = UINT64_MAX;
+    auto drain = [&](Slot& s) -> int {
+        if (!s.busy) return PCS_OK;
+        hipError_t err = hipStreamSynchronize(s.stream);
+        s.busy = false;
+        if (err != hipSuccess) return hip_fail(err, "hipStreamSynchronize");
+        for (uint64_t i = 0; i < s.count; ++i) {
+            const uint64_t gi = s.first + i;
+            if (mode == 1) {
+                out_ok[gi] = s.h_ok[i];
+                if (!s.h_ok[i] && gi < bad) bad = gi;
+            } else if (mode == 2) {
+                std::memcpy(const_cast<void*>(pages[gi]), &s.h_dig[i], 8);  // EncodeFixed64 (LE)
+            } else {
+                out_dig[gi] = s.h_dig[i];
+            }
+        }
+        return PCS_OK;
+    };
+
+    int rc = PCS_OK;
+    uint64_t k = 0;
+    for (uint64_t first = 0; first < n && rc == PCS_OK; first += chunk, ++k) {
+        Slot& s = ctx.slot[k & 1];
+        if ((rc = drain(s))) break;
+        const uint64_t cnt = std::min(chunk, n - first);
+        for (uint64_t i = 0; i < cnt; ++i) std::memcpy(s.h_pages + i * P, pages[first + i], P);
+        s.first = first;
+        s.count = cnt;
+        e = hipMemcpyAsync(s.d_pages, s.h_pages, cnt * P, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess)
+            e = pcs::run_pages(mode == 1 ? 1 : 0, algo, s.d_pages, P, cnt, s.d_dig, s.d_ok, nullptr, s.stream);
+        if (e == hipErrorNotSupported) {
+            (void)hipGetLastError();
+            // staging is 256-byte aligned, so only an odd page size lands here
+            rc = pages_common(mode == 1 ? 1 : 0, s.d_pages, P, cnt, algo, s.d_dig, s.d_ok, nullptr,
+                              reinterpret_cast<pcs_stream_t>(s.stream));
+            if (rc) break;
+            e = hipSuccess;
+        }
+        if (e == hipSuccess) {
+            if (mode == 1) e = hipMemcpyAsync(s.h_ok, s.d_ok, cnt, hipMemcpyDeviceToHost, s.stream);
+            else e = hipMemcpyAsync(s.h_dig, s.d_dig, cnt * 8, hipMemcpyDeviceToHost, s.stream);
+        }
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "host batch enqueue");
+            break;
+        }
+        s.busy = true;
+    }
+    for (auto& s : ctx.slot) {
+        const int r2 = drain(s);
+        if (!rc) rc = r2;
+    }
+    if (first_bad) *first_bad = bad;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pcs_version(void) { return "eloqstore-pcs 0.1.0 (gfx950; xxHash v0.8.3 page path)"; }
+
+const char* pcs_last_error(void) { return t_last_error.c_str(); }
+
+int pcs_device_count(int* count) {
+    if (!count) return fail(PCS_ERR_INVALID, "count is null");
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    *count = (e == hipSuccess) ? n : 0;
+    return e == hipSuccess ? PCS_OK : fail(PCS_ERR_NO_DEVICE, hipGetErrorString(e));
+}
+
+int pcs_set_device(int device) {
+    if (int rc = require_device()) return rc;
+    return finish(hipSetDevice(device), "hipSetDevice");
+}
+
+int pcs_synchronize(pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    return finish(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)), "hipStreamSynchronize");
+}
+
+int pcs_pages_digest_dev(const void* d_pages, uint64_t page_size, uint64_t n_pages, int algo, uint64_t* d_digests,
+                         pcs_stream_t stream) {
+    return pages_common(0, d_pages, page_size, n_pages, algo, d_digests, nullptr, nullptr, stream);
+}
+
+int pcs_pages_validate_dev(const void* d_pages, uint64_t page_size, uint64_t n_pages, int algo, uint8_t* d_ok,
+                           uint64_t* d_first_bad, pcs_stream_t stream) {
+    return pages_common(1, d_pages, page_size, n_pages, algo, nullptr, d_ok, d_first_bad, stream);
+}
+
+int pcs_pages_stamp_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, int algo, pcs_stream_t stream) {
+    return pages_common(2, d_pages, page_size, n_pages, algo, nullptr, nullptr, nullptr, stream);
+}
+
+int pcs_desc_digest_dev(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, int algo,
+                        uint64_t* d_digests, pcs_stream_t stream) {
+    return desc_common(0, d_base, d_off, d_len, n, algo, 8, 0, d_digests, nullptr, nullptr, stream);
+}
+
+int pcs_desc_validate_dev(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, int algo,
+                          uint8_t* d_ok, uint64_t* d_first_bad, pcs_stream_t stream) {
+    return desc_common(1, d_base, d_off, d_len, n, algo, 8, 0, nullptr, d_ok, d_first_bad, stream);
+}
+
+int pcs_desc_stamp_dev(void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, int algo,
+                       pcs_stream_t stream) {
+    return desc_common(2, d_base, d_off, d_len, n, algo, 8, 0, nullptr, nullptr, nullptr, stream);
+}
+
+int pcs_xxh3_64_ranges_dev(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n,
+                           uint64_t* d_out, pcs_stream_t stream) {
+    return desc_common(0, d_base, d_off, d_len, n, PCS_XXH3_64, 0, 0, d_out, nullptr, nullptr, stream);
+}
+
+int pcs_xxh64_ranges_dev(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, uint64_t seed,
+                         uint64_t* d_out, pcs_stream_t stream) {
+    return desc_common(0, d_base, d_off, d_len, n, PCS_XXH64, 0, seed, d_out, nullptr, nullptr, stream);
+}
+
+int pcs_pages_validate_host(const void* const* pages, uint64_t page_size, uint64_t n_pages, int algo, uint8_t* ok,
+                            uint64_t* first_bad) {
+    if (n_pages && !ok) return fail(PCS_ERR_INVALID, "ok is null");
+    return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
+}
+
+int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_pages, int algo) {
+    return host_batch(2, const_cast<const void* const*>(pages), page_size, n_pages, algo, nullptr, nullptr, nullptr);
+}
+
+int pcs_pages_digest_host(const void* const* pages, uint64_t page_size, uint64_t n_pages, int algo,
+                          uint64_t* digests) {
+    if (n_pages && !digests) return fail(PCS_ERR_INVALID, "digests is null");
+    return host_batch(0, pages, page_size, n_pages, algo, nullptr, nullptr, digests);
+}
+
+int pcs_shard_range(uint64_t n, int world, int rank, uint64_t* begin, uint64_t* end) {
+    if (!begin || !end) return fail(PCS_ERR_INVALID, "begin/end is null");
+    if (world <= 0 || rank < 0 || rank >= world) return fail(PCS_ERR_INVALID, "rank must be in [0, world)");
+    const unsigned __int128 N = n;
+    *begin = (uint64_t)(N * (unsigned)rank / (unsigned)world);
+    *end = (uint64_t)(N * (unsigned)(rank + 1) / (unsigned)world);
+    return PCS_OK;
+}
+
+int pcs_gen_pages_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t seed, uint64_t first_page_index,
+                      pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (page_size == 0 || page_size % 8) return fail(PCS_ERR_INVALID, "page_size must be a positive multiple of 8");
+    if (n_pages && !d_pages) return fail(PCS_ERR_INVALID, "d_pages is null");
+    return finish(pcs::run_gen_pages(static_cast<uint8_t*>(d_pages), page_size, n_pages, seed, first_page_index,
+                                     reinterpret_cast<hipStream_t>(stream)),
+                  "gen kernel launch");
+}
+
+int pcs_gen_desc_dev(void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, uint64_t seed,
+                     uint64_t first_page_index, pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (n && (!d_base || !d_off || !d_len)) return fail(PCS_ERR_INVALID, "null descriptor pointer");
+    return finish(pcs::run_gen_desc(static_cast<uint8_t*>(d_base), d_off, d_len, n, seed, first_page_index,
+                                    reinterpret_cast<hipStream_t>(stream)),
+                  "gen kernel launch");
+}
+
+int pcs_flip_byte_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t every, uint64_t byte_offset,
+                      pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (every == 0 || byte_offset >= page_size) return fail(PCS_ERR_INVALID, "every must be > 0, byte_offset < page_size");
+    if (n_pages && !d_pages) return fail(PCS_ERR_INVALID, "d_pages is null");
+    return finish(pcs::run_flip(static_cast<uint8_t*>(d_pages), page_size, n_pages, every, byte_offset,
+                                reinterpret_cast<hipStream_t>(stream)),
+                  "flip kernel launch");
+}
+
+int pcs_read_ceiling_dev(const void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t* d_out,
+                         pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (n_pages && (!d_pages || !d_out)) return fail(PCS_ERR_INVALID, "null pointer");
+    const hipError_t e = pcs::run_read_ceiling(static_cast<const uint8_t*>(d_pages), page_size, n_pages, d_out,
+                                               reinterpret_cast<hipStream_t>(stream));
+    if (e == hipErrorNotSupported) return fail(PCS_ERR_INVALID, "page_size must be a power of two in [256, 65536]");
+    return finish(e, "read-ceiling kernel launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,769 @@
+// pcs_kernels.hip — hand-written CDNA4 (gfx950) kernels for EloqStore's page
+// checksum path: XXH3_64bits(page + 8, P - 8) / XXH64(page + 8, P - 8, 0) over
+// many independent pages per launch (reference call sites:
+// src/storage/page.cpp:18-31, src/async_io_manager.cpp:239-244 / 353-366,
+// src/tasks/write_task.cpp:58-79).
+//
+// Work decomposition:
+//
+//   XXH3 long path — one 16-lane DPP row ("group") per page, 4 pages per wave.
+//     Chunk c of a 1 KiB input block is 256 page bytes; lane g of the group
+//     loads page bytes [blk*1024 + 256c + 16g, +16) with one global_load_dwordx4,
+//     so a wave-instruction reads four fully-used 256 B segments.  Inside an
+//     XXH3 block the accumulator updates are pure mod-2^64 sums (xxhash.h:5778-
+//     5817), so each lane folds its words into four partial sums and a block
+//     needs one cross-lane reduction: a DPP row_ror:15 exchange (page words sit
+//     one u64 ahead of the 8-byte-offset hashed stripes) plus row_ror 4/8 folds.
+//     The per-block scramble (xxhash.h:5827-5856) runs redundantly on every lane
+//     for the accumulator pair (2p, 2p+1), p = g & 3; the merge (xxhash.h:6029-
+//     6062) folds the four pairs with row_ror 1/2.
+//   XXH64 — one quad per page (lane a owns accumulator a), 16 pages per wave;
+//     the serial round chain of each accumulator stays in one lane.
+//   Generic — one lane per input range, any length (all XXH3 length classes,
+//     xxhash.h:4641-4856), for odd-sized descriptors and raw ranges.
+#include "xxh_device.h"
+#include "eloqstore_pcs_internal.h"
+
+#include <mutex>
+
+namespace pcs {
+
+// ---------------------------------------------------------------------------
+// secret-derived key tables (all offsets fixed by xxhash.h)
+// ---------------------------------------------------------------------------
+struct KeyTables {
+    uint64_t acc[24];   // secret + 8k       accumulate (stripe s, lane l -> k = s + l), :5801
+    uint64_t last[8];   // secret + 121 + 8l last stripe (XXH_SECRET_LASTACC_START 7), :6013-6015
+    uint64_t scr[8];    // secret + 128 + 8l scramble (secret + secretSize - 64), :5996
+    uint64_t merge[8];  // secret + 11 + 8m  mergeAccs (XXH_SECRET_MERGEACCS_START), :6056-6061
+};
+constexpr KeyTables make_tables() {
+    KeyTables t{};
+    for (int k = 0; k < 24; ++k) t.acc[k] = secret64(8 * k);
+    for (int l = 0; l < 8; ++l) t.last[l] = secret64(121 + 8 * l);
+    for (int l = 0; l < 8; ++l) t.scr[l] = secret64(128 + 8 * l);
+    for (int m = 0; m < 8; ++m) t.merge[m] = secret64(11 + 8 * m);
+    return t;
+}
+__constant__ KeyTables c_keys = make_tables();
+
+// XXH3_INIT_ACC (xxhash.h:6064-6065)
+__constant__ uint64_t c_init_acc[8] = {kP32_3, kP64_1, kP64_2, kP64_3, kP64_4, kP32_2, kP64_5, kP32_1};
+
+enum Mode : int { kDigest = 0, kValidate = 1, kStamp = 2 };
+
+// Per-page output for every kernel: digest array, verdict array + first bad
+// index, or the digest stamped little-endian into page bytes [0, 8).
+__device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_t stored, uint8_t* page_w,
+                                     uint64_t* out, uint8_t* ok, unsigned long long* first_bad) {
+    if (mode == kStamp) {
+        *reinterpret_cast<uint64_t*>(page_w) = h;
+        if (out) out[idx] = h;
+    } else if (mode == kValidate) {
+        const bool good = (h == stored);
+        ok[idx] = good ? 1 : 0;
+        if (out) out[idx] = h;
+        if (!good && first_bad) atomicMin(first_bad, (unsigned long long)idx);
+    } else {
+        out[idx] = h;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// XXH3 long-input page hash, one 16-lane group per page
+// ---------------------------------------------------------------------------
+//
+// Index bookkeeping.  Page word w (u64) is input word j = w - 1 (the digest
+// occupies page word 0).  Within a 1 KiB input block, input word jb sits in
+// stripe s = jb >> 3, accumulator lane l = jb & 7, and is keyed with secret
+// word k = s + l.  Lane g, chunk c, half e holds page word 128b + 32c + 2g + e,
+// i.e. jb = 32c + 2g + e - 1:
+//   e = 0 -> l odd  (pair (g-1) & 3): multiply term to the odd slot, raw add
+//            to the even slot ("U" sums);
+//   e = 1 -> l even (pair g & 3):     multiply term to the even slot, raw add
+//            to the odd slot ("V" sums).
+// The one word with jb = -1 (lane 0, chunk 0, e = 0) is page word 128b: it
+// belongs to the PREVIOUS block (or is the stored digest for b = 0).  Lane 0
+// instead takes page word 128(b+1) ("carry"), the block's own last input word
+// (stripe 15, lane 7, key 22), read by a separate 8-byte load.
+struct Xxh3Lane {
+    uint64_t k[4][2];     // accumulate keys, chunk c, half e
+    uint64_t kl0, kl1;    // last-stripe keys (used by lanes 12..15)
+    uint64_t ks_e, ks_o;  // scramble keys for pair p
+    uint64_t km_e, km_o;  // merge keys for pair p
+    uint64_t init_e, init_o;
+    int g;
+};
+
+__device__ __forceinline__ Xxh3Lane make_xxh3_lane(int g) {
+    Xxh3Lane L;
+    L.g = g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            int jb = 32 * c + 2 * g + e - 1;
+            if (jb < 0) jb = 127;  // lane 0's carry word
+            L.k[c][e] = c_keys.acc[(jb >> 3) + (jb & 7)];
+        }
+    const int gl = g & 3;
+    L.kl0 = c_keys.last[2 * gl];
+    L.kl1 = c_keys.last[2 * gl + 1];
+    L.ks_e = c_keys.scr[2 * gl];
+    L.ks_o = c_keys.scr[2 * gl + 1];
+    L.km_e = c_keys.merge[2 * gl];
+    L.km_o = c_keys.merge[2 * gl + 1];
+    L.init_e = c_init_acc[2 * gl];
+    L.init_o = c_init_acc[2 * gl + 1];
+    return L;
+}
+
+// Fold one 1 KiB block (chunks 0..nchunks-1 present) into the sums (Te, To)
+// of accumulator pair g & 3.  FINAL marks the last, partial block: no carry
+// word, the last stripe (page words P/8-8 .. P/8-1, held by lanes 12..15 of
+// the final chunk) keyed with secret + 121, and page words P/8-7 .. P/8-1
+// excluded from the ordinary stripes (xxhash.h:6005-6016).
+template <bool FINAL>
+__device__ __forceinline__ void xxh3_block_terms(const Xxh3Lane& L, const uint4 (&d)[4], uint64_t carry,
+                                                 int nchunks, uint64_t& Te, uint64_t& To) {
+    uint64_t Ue = 0, Uo = 0, Ve = 0, Vo = 0;
+    const int g = L.g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (FINAL && c >= nchunks) break;
+        uint64_t w0 = ((uint64_t)d[c].y << 32) | d[c].x;
+        const uint64_t w1 = ((uint64_t)d[c].w << 32) | d[c].z;
+        bool use0 = true, use1 = true;
+        if (c == 0) {
+            if (FINAL) use0 = (g != 0);
+            else w0 = (g == 0) ? carry : w0;
+        }
+        if (FINAL && c == nchunks - 1 && g >= 12) {
+            use1 = false;
+            use0 = use0 && (g == 12);
+            // last-stripe lane l' = 2(g-12) + e: both halves land on pair g & 3
+            Ve += mul32x32(w0 ^ L.kl0) + w1;
+            Vo += mul32x32(w1 ^ L.kl1) + w0;
+        }
+        const uint64_t m0 = mul32x32(w0 ^ L.k[c][0]);
+        const uint64_t m1 = mul32x32(w1 ^ L.k[c][1]);
+        Uo += use0 ? m0 : 0;
+        Ue += use0 ? w0 : 0;
+        Ve += use1 ? m1 : 0;
+        Vo += use1 ? w1 : 0;
+    }
+    // pair p = g & 3 collects V of lanes g = p (mod 4) and U of lanes g = p + 1
+    Te = Ve + dpp64<kRowRor15>(Ue);
+    To = Vo + dpp64<kRowRor15>(Uo);
+    Te += dpp64<kRowRor4>(Te);
+    To += dpp64<kRowRor4>(To);
+    Te += dpp64<kRowRor8>(Te);
+    To += dpp64<kRowRor8>(To);
+}
+
+__device__ __forceinline__ uint64_t xxh3_merge(const Xxh3Lane& L, uint64_t Ae, uint64_t Ao, uint64_t len) {
+    uint64_t m = mul_fold64(Ae ^ L.km_e, Ao ^ L.km_o);
+    m += dpp64<kRowRor1>(m);
+    m += dpp64<kRowRor2>(m);
+    return xxh3_avalanche(len * kP64_1 + m);
+}
+
+// Whole page, compile-time page size P (P % 256 == 0, P >= 256).  Blocks are
+// loaded in batches of up to 4 (4 KiB per page, 16 KiB per wave in flight)
+// before any of them is folded, so a 4 KiB page is one batch.
+template <int P>
+__device__ __forceinline__ uint64_t xxh3_page_fixed(const uint8_t* __restrict__ page, const Xxh3Lane& L,
+                                                    uint64_t& stored) {
+    constexpr int NB = (P - 9) / 1024;   // full blocks (xxhash.h:5996)
+    constexpr int R = P / 256 - 4 * NB;  // chunks in the final block, 1..4
+    constexpr int TB = NB + 1;
+    const uint4* base = reinterpret_cast<const uint4*>(page) + L.g;
+    uint64_t Ae = L.init_e, Ao = L.init_o;
+#pragma unroll
+    for (int b0 = 0; b0 < TB; b0 += 4) {
+        uint4 d[4][4];
+        uint64_t carry[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int b = b0 + i;
+            if (b >= TB) break;
+            const int nc = (b == NB) ? R : 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < nc) d[i][c] = base[b * 64 + c * 16];
+            if (b < NB) carry[i] = *reinterpret_cast<const uint64_t*>(page + (b + 1) * 1024);
+        }
+        if (b0 == 0) stored = ((uint64_t)d[0][0].y << 32) | d[0][0].x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int b = b0 + i;
+            if (b >= TB) break;
+            uint64_t Te, To;
+            if (b < NB) {
+                xxh3_block_terms<false>(L, d[i], carry[i], 4, Te, To);
+                Ae = xxh3_scramble(Ae + Te, L.ks_e);
+                Ao = xxh3_scramble(Ao + To, L.ks_o);
+            } else {
+                xxh3_block_terms<true>(L, d[i], 0, R, Te, To);
+                Ae += Te;
+                Ao += To;
+            }
+        }
+    }
+    return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
+}
+
+// Run-time page size (P % 256 == 0, P >= 256): one block per step.
+__device__ __forceinline__ uint64_t xxh3_page_rt(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
+                                                 uint64_t& stored) {
+    const int NB = (int)((P - 9) / 1024);
+    const int R = (int)(P / 256) - 4 * NB;
+    const uint4* base = reinterpret_cast<const uint4*>(page) + L.g;
+    uint64_t Ae = L.init_e, Ao = L.init_o;
+    stored = *reinterpret_cast<const uint64_t*>(page);
+    for (int b = 0; b < NB; ++b) {
+        uint4 d[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[c] = base[b * 64 + c * 16];
+        const uint64_t carry = *reinterpret_cast<const uint64_t*>(page + (size_t)(b + 1) * 1024);
+        uint64_t Te, To;
+        xxh3_block_terms<false>(L, d, carry, 4, Te, To);
+        Ae = xxh3_scramble(Ae + Te, L.ks_e);
+        Ao = xxh3_scramble(Ao + To, L.ks_o);
+    }
+    uint4 d[4] = {};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if (c < R) d[c] = base[NB * 64 + c * 16];
+    uint64_t Te, To;
+    xxh3_block_terms<true>(L, d, 0, R, Te, To);
+    return xxh3_merge(L, Ae + Te, Ao + To, (uint64_t)(P - 8));
+}
+
+__device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
+    return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
+}
+
+template <int P, int MODE>
+__global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
+                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                   unsigned long long* first_bad) {
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
+    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+        const uint8_t* page = pages + pg * (uint64_t)P;
+        uint64_t stored = 0;
+        const uint64_t h = xxh3_page_fixed<P>(page, L, stored);
+        if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+    }
+}
+
+// Fixed stride, run-time page size.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
+                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                    unsigned long long* first_bad) {
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
+    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+        const uint8_t* page = pages + pg * (uint64_t)P;
+        uint64_t stored = 0;
+        const uint64_t h = xxh3_page_rt(page, P, L, stored);
+        if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+    }
+}
+
+// Descriptor batch (mixed sizes).  Pages that miss the fast-path shape are
+// left to k_generic_desc.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ len, uint64_t n,
+                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                  unsigned long long* first_bad) {
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
+    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+        const uint64_t o = off[pg];
+        const uint32_t P = len[pg];
+        if (!xxh3_fast_ok(o, P)) continue;
+        const uint8_t* page = base + o;
+        uint64_t stored = 0;
+        const uint64_t h = xxh3_page_rt(page, P, L, stored);
+        if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// XXH64 page hash, one quad per page (lane a = accumulator a)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t xxh64_init(int a) {
+    // XXH64_initAccs with seed 0 (xxhash.h:3521-3528)
+    return a == 0 ? kP64_1 + kP64_2 : a == 1 ? kP64_2 : a == 2 ? 0ull : (uint64_t)0 - kP64_1;
+}
+
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+
+// XXH64_finalize (xxhash.h:3611-3634) over the (len & 31) bytes at tail.
+__device__ __forceinline__ uint64_t xxh64_tail(uint64_t h, const uint8_t* tail, uint64_t len) {
+    uint32_t rem = (uint32_t)(len & 31);
+    for (; rem >= 8; rem -= 8, tail += 8) {
+        h ^= xxh64_round(0, ld64(tail));
+        h = rotl64(h, 27) * kP64_1 + kP64_4;
+    }
+    if (rem >= 4) {
+        h ^= (uint64_t)ld32(tail) * kP64_1;
+        h = rotl64(h, 23) * kP64_2 + kP64_3;
+        rem -= 4;
+        tail += 4;
+    }
+    for (; rem > 0; --rem, ++tail) {
+        h ^= (uint64_t)(*tail) * kP64_5;
+        h = rotl64(h, 11) * kP64_1;
+    }
+    return xxh64_avalanche(h);
+}
+
+// XXH64_mergeAccs (xxhash.h:3573-3593) for a quad whose lane a holds acc a.
+__device__ __forceinline__ uint64_t xxh64_quad_merge(uint64_t v) {
+    const uint64_t v0 = dpp64<quad_bcast(0)>(v);
+    const uint64_t v1 = dpp64<quad_bcast(1)>(v);
+    const uint64_t v2 = dpp64<quad_bcast(2)>(v);
+    const uint64_t v3 = dpp64<quad_bcast(3)>(v);
+    uint64_t h = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
+    h = (h ^ xxh64_round(0, v0)) * kP64_1 + kP64_4;
+    h = (h ^ xxh64_round(0, v1)) * kP64_1 + kP64_4;
+    h = (h ^ xxh64_round(0, v2)) * kP64_1 + kP64_4;
+    h = (h ^ xxh64_round(0, v3)) * kP64_1 + kP64_4;
+    return h;
+}
+
+// Page convention: XXH64 over [8, P).  Needs 8-byte aligned page, P % 8 == 0,
+// P >= 40 (so the hashed length is >= 32 and the 4-accumulator loop runs).
+constexpr int kX64Unroll = 16;
+__device__ __forceinline__ uint64_t xxh64_page(const uint8_t* __restrict__ page, uint32_t P, int a,
+                                               uint64_t& stored) {
+    const uint64_t len = P - 8;
+    const uint32_t ns = (uint32_t)(len / 32);
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(page + 8) + a;
+    stored = *reinterpret_cast<const uint64_t*>(page);
+    uint64_t v = xxh64_init(a);
+    uint32_t s = 0;
+    for (; s + kX64Unroll <= ns; s += kX64Unroll) {
+        uint64_t x[kX64Unroll];
+#pragma unroll
+        for (int u = 0; u < kX64Unroll; ++u) x[u] = w[4 * (s + u)];
+#pragma unroll
+        for (int u = 0; u < kX64Unroll; ++u) v = xxh64_round(v, x[u]);
+    }
+    for (; s < ns; ++s) v = xxh64_round(v, w[4 * s]);
+    const uint64_t h = xxh64_quad_merge(v) + len;
+    return xxh64_tail(h, page + 8 + 32 * (uint64_t)ns, len);
+}
+
+__device__ __forceinline__ bool xxh64_fast_ok(uint64_t off, uint32_t P) {
+    return (P % 8u) == 0 && P >= 40u && (off % 8u) == 0;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
+                                                     uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                     unsigned long long* first_bad) {
+    const int a = threadIdx.x & 3;
+    const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x >> 2);
+    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; pg < n; pg += nquads) {
+        const uint8_t* page = pages + pg * (uint64_t)P;
+        uint64_t stored = 0;
+        const uint64_t h = xxh64_page(page, P, a, stored);
+        if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ len, uint64_t n,
+                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                   unsigned long long* first_bad) {
+    const int a = threadIdx.x & 3;
+    const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x >> 2);
+    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; pg < n; pg += nquads) {
+        const uint64_t o = off[pg];
+        const uint32_t P = len[pg];
+        if (!xxh64_fast_ok(o, P)) continue;
+        const uint8_t* page = base + o;
+        uint64_t stored = 0;
+        const uint64_t h = xxh64_page(page, P, a, stored);
+        if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// generic single-lane XXH3_64bits / XXH64 over any byte range (any alignment)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rrmxmx(uint64_t h, uint64_t len) {  // xxhash.h:4595-4603
+    h ^= rotl64(h, 49) ^ rotl64(h, 24);
+    h *= kMX2;
+    h ^= (h >> 35) + len;
+    h *= kMX2;
+    return h ^ (h >> 28);
+}
+
+// XXH3_mix16B, seed 0 (xxhash.h:4740-4763); SOFF is a compile-time secret offset
+__device__ __forceinline__ uint64_t mix16(const uint8_t* in, uint64_t k0, uint64_t k1) {
+    return mul_fold64(ld64(in) ^ k0, ld64(in + 8) ^ k1);
+}
+
+__device__ uint64_t xxh3_any(const uint8_t* in, uint64_t len) {
+    if (len <= 16) {  // XXH3_len_0to16_64b, :4696-4704
+        if (len > 8) {
+            const uint64_t lo = ld64(in) ^ (secret64(24) ^ secret64(32));
+            const uint64_t hi = ld64(in + len - 8) ^ (secret64(40) ^ secret64(48));
+            const uint64_t acc = len + __builtin_bswap64(lo) + hi + mul_fold64(lo, hi);
+            return xxh3_avalanche(acc);
+        }
+        if (len >= 4) {
+            const uint64_t in1 = ld32(in), in2 = ld32(in + len - 4);
+            const uint64_t keyed = (in2 + (in1 << 32)) ^ (secret64(8) ^ secret64(16));
+            return rrmxmx(keyed, len);
+        }
+        if (len > 0) {
+            const uint32_t combined = ((uint32_t)in[0] << 16) | ((uint32_t)in[len >> 1] << 24) |
+                                      (uint32_t)in[len - 1] | ((uint32_t)len << 8);
+            return xxh64_avalanche((uint64_t)combined ^ (uint64_t)(secret32(0) ^ secret32(4)));
+        }
+        return xxh64_avalanche(secret64(56) ^ secret64(64));
+    }
+    if (len <= 128) {  // XXH3_len_17to128_64b, :4766-4799
+        uint64_t acc = len * kP64_1;
+        const int rounds = (int)((len - 1) / 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i > rounds) break;
+            acc += mix16(in + 16 * i, secret64(32 * i), secret64(32 * i + 8));
+            acc += mix16(in + len - 16 * (i + 1), secret64(32 * i + 16), secret64(32 * i + 24));
+        }
+        return xxh3_avalanche(acc);
+    }
+    if (len <= 240) {  // XXH3_len_129to240_64b, :4802-4856
+        uint64_t acc = len * kP64_1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += mix16(in + 16 * i, secret64(16 * i), secret64(16 * i + 8));
+        acc = xxh3_avalanche(acc);
+        uint64_t tail = mix16(in + len - 16, secret64(119), secret64(127));
+        const int rounds = (int)(len / 16);
+#pragma unroll
+        for (int i = 8; i < 15; ++i) {
+            if (i >= rounds) break;
+            tail += mix16(in + 16 * i, secret64(16 * (i - 8) + 3), secret64(16 * (i - 8) + 11));
+        }
+        return xxh3_avalanche(acc + tail);
+    }
+    // long input, scalar (xxhash.h:5988-6081)
+    uint64_t acc[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[l] = c_init_acc[l];
+    const uint64_t blocks = (len - 1) / 1024;
+    auto stripe = [&](const uint8_t* p, int koff, bool last) {
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const uint64_t v = ld64(p + 8 * l);
+            const uint64_t k = v ^ (last ? c_keys.last[l] : c_keys.acc[koff + l]);
+            acc[l ^ 1] += v;
+            acc[l] += mul32x32(k);
+        }
+    };
+    for (uint64_t b = 0; b < blocks; ++b) {
+        for (int s = 0; s < 16; ++s) stripe(in + 1024 * b + 64 * s, s, false);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[l] = xxh3_scramble(acc[l], c_keys.scr[l]);
+    }
+    const int ns = (int)(((len - 1) - 1024 * blocks) / 64);
+    for (int s = 0; s < ns; ++s) stripe(in + 1024 * blocks + 64 * s, s, false);
+    stripe(in + len - 64, 0, true);
+    uint64_t r = len * kP64_1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r += mul_fold64(acc[2 * i] ^ c_keys.merge[2 * i], acc[2 * i + 1] ^ c_keys.merge[2 * i + 1]);
+    return xxh3_avalanche(r);
+}
+
+__device__ uint64_t xxh64_any(const uint8_t* p, uint64_t len, uint64_t seed) {  // xxhash.h:3655-3673
+    uint64_t h;
+    const uint8_t* q = p;
+    if (len >= 32) {
+        uint64_t v[4] = {seed + kP64_1 + kP64_2, seed + kP64_2, seed, seed - kP64_1};
+        const uint64_t ns = len / 32;
+        for (uint64_t s = 0; s < ns; ++s, q += 32)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = xxh64_round(v[i], ld64(q + 8 * i));
+        h = rotl64(v[0], 1) + rotl64(v[1], 7) + rotl64(v[2], 12) + rotl64(v[3], 18);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h = (h ^ xxh64_round(0, v[i])) * kP64_1 + kP64_4;
+    } else {
+        h = seed + kP64_5;
+    }
+    return xxh64_tail(h + len, q, len);
+}
+
+// One lane per range.  SKIP = 8 applies the page convention (hash [8, len),
+// stored digest in [0, 8)); SKIP = 0 hashes the raw range.  With FILTER set,
+// ranges the fast kernels handle are skipped.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ len, uint64_t n, int algo,
+                                                     uint64_t seed, int skip, int filter, uint64_t* __restrict__ out,
+                                                     uint8_t* __restrict__ ok, unsigned long long* first_bad) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t o = off[i];
+        const uint32_t L = len[i];
+        if (filter && (algo == 0 ? xxh3_fast_ok(o, L) : xxh64_fast_ok(o, L))) continue;
+        const uint8_t* p = base + o;
+        if ((uint32_t)skip > L) {  // page shorter than its digest header: never valid
+            if (MODE == kValidate) {
+                ok[i] = 0;
+                if (out) out[i] = 0;
+                if (first_bad) atomicMin(first_bad, (unsigned long long)i);
+            } else if (MODE == kDigest) {
+                out[i] = 0;
+            }
+            continue;
+        }
+        const uint64_t h = algo == 0 ? xxh3_any(p + skip, L - skip) : xxh64_any(p + skip, L - skip, seed);
+        const uint64_t stored = skip ? ld64(p) : 0;
+        if (MODE == kStamp) {
+            __builtin_memcpy(const_cast<uint8_t*>(p), &h, 8);
+            if (out) out[i] = h;
+        } else {
+            emit(MODE, i, h, stored, nullptr, out, ok, first_bad);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// workload generation / corruption / read-ceiling (benchmark + test tooling)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t page, uint64_t w) {
+    uint64_t z = (seed ^ page) + (w + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_gen_pages(uint64_t* __restrict__ pages, uint64_t words_per_page, uint64_t n,
+                                                  uint64_t seed, uint64_t first_page) {
+    for (uint64_t p = blockIdx.x; p < n; p += gridDim.x) {
+        uint64_t* dst = pages + p * words_per_page;
+        for (uint64_t w = threadIdx.x; w < words_per_page; w += blockDim.x)
+            dst[w] = splitmix_word(seed, first_page + p, w);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gen_desc(uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ len, uint64_t n, uint64_t seed,
+                                                 uint64_t first_page) {
+    for (uint64_t p = blockIdx.x; p < n; p += gridDim.x) {
+        uint8_t* dst = base + off[p];
+        const uint32_t L = len[p];
+        for (uint32_t w = threadIdx.x; w * 8u < L; w += blockDim.x) {
+            const uint64_t v = splitmix_word(seed, first_page + p, w);
+            const uint32_t nb = (L - w * 8u) < 8u ? (L - w * 8u) : 8u;
+            if (nb == 8 && ((off[p] & 7) == 0)) *reinterpret_cast<uint64_t*>(dst + 8u * w) = v;
+            else
+                for (uint32_t b = 0; b < nb; ++b) dst[8u * w + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+}
+
+__global__ void k_flip_byte(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint64_t byte_off) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p = k * every;
+    if (p < n) pages[p * P + byte_off] ^= 0xFF;
+}
+
+// Same access pattern and output as k_xxh3_fixed<P, kDigest> minus the hash:
+// the achievable HBM read rate for this layout (roofline "measured ceiling").
+template <int P>
+__global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
+                                                     uint64_t* __restrict__ out) {
+    const int g = threadIdx.x & 15;
+    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
+    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+        const uint4* base = reinterpret_cast<const uint4*>(pages + pg * (uint64_t)P) + g;
+        uint32_t x = 0, y = 0, z = 0, w = 0;
+#pragma unroll
+        for (int c = 0; c < P / 256; ++c) {
+            const uint4 v = base[c * 16];
+            x ^= v.x; y += v.y; z ^= v.z; w += v.w;
+        }
+        uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + w);
+        r ^= dpp64<kRowRor1>(r);
+        r ^= dpp64<kRowRor2>(r);
+        r ^= dpp64<kRowRor4>(r);
+        r ^= dpp64<kRowRor8>(r);
+        if (g == 0) out[pg] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launch plumbing
+// ---------------------------------------------------------------------------
+namespace {
+
+int g_cu_count[64];
+std::once_flag g_cu_once[64];
+
+int cu_count() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    std::call_once(g_cu_once[dev], [dev] {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        g_cu_count[dev] = cus;
+    });
+    return g_cu_count[dev];
+}
+
+// Grid for a grid-stride kernel: enough 256-thread blocks to cover the work,
+// capped at blocks_per_cu resident blocks per CU.
+unsigned grid_for(uint64_t units, unsigned units_per_block, unsigned blocks_per_cu) {
+    const uint64_t need = (units + units_per_block - 1) / units_per_block;
+    const uint64_t cap = (uint64_t)cu_count() * blocks_per_cu;
+    return (unsigned)(need < cap ? (need ? need : 1) : cap);
+}
+
+constexpr unsigned kBlock = 256;
+constexpr unsigned kBlocksPerCu = 8;
+
+template <int MODE>
+hipError_t launch_xxh3_fixed(int P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
+                             unsigned long long* fb, hipStream_t s) {
+    const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
+    switch (P) {
+#define CASE(SZ) \
+    case SZ: hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb); break;
+        CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
+#undef CASE
+        default:
+            hipLaunchKernelGGL((k_xxh3_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok,
+                               fb);
+    }
+    return hipGetLastError();
+}
+
+bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) == 0; }
+
+}  // namespace
+
+// Fixed-stride pages.  Shape checks are done by the caller (capi).
+template <int MODE>
+static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
+                             unsigned long long* fb, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const bool aligned16 = ((uintptr_t)pages % 16) == 0;
+    const bool aligned8 = ((uintptr_t)pages % 8) == 0;
+    if (algo == 0 && aligned16 && P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull) {
+        if (is_pow2_page(P)) return launch_xxh3_fixed<MODE>((int)P, pages, n, out, ok, fb, s);
+        const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
+        hipLaunchKernelGGL((k_xxh3_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
+        return hipGetLastError();
+    }
+    if (algo == 1 && aligned8 && P % 8 == 0 && P >= 40 && P <= 0xFFFFFFFFull) {
+        const unsigned grid = grid_for(n, kBlock / 4, kBlocksPerCu);
+        hipLaunchKernelGGL((k_xxh64_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
+        return hipGetLastError();
+    }
+    return hipErrorNotSupported;  // caller falls back to the descriptor path
+}
+
+hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
+                     unsigned long long* fb, hipStream_t s) {
+    switch (mode) {
+        case kDigest: return pages_impl<kDigest>(algo, pages, P, n, out, ok, fb, s);
+        case kValidate: return pages_impl<kValidate>(algo, pages, P, n, out, ok, fb, s);
+        default: return pages_impl<kStamp>(algo, pages, P, n, out, ok, fb, s);
+    }
+}
+
+template <int MODE>
+static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
+                            int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* fb,
+                            hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (skip == 8 && seed == 0) {
+        // fast kernels for conforming pages, generic lanes for the rest
+        if (algo == 0) {
+            const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
+            hipLaunchKernelGGL((k_xxh3_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+        } else {
+            const unsigned grid = grid_for(n, kBlock / 4, kBlocksPerCu);
+            hipLaunchKernelGGL((k_xxh64_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const unsigned grid = grid_for(n, kBlock, kBlocksPerCu);
+        hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip,
+                           1, out, ok, fb);
+        return hipGetLastError();
+    }
+    const unsigned grid = grid_for(n, kBlock, kBlocksPerCu);
+    hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip, 0,
+                       out, ok, fb);
+    return hipGetLastError();
+}
+
+hipError_t run_desc(int mode, int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
+                    int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* fb, hipStream_t s) {
+    switch (mode) {
+        case kDigest: return desc_impl<kDigest>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
+        case kValidate: return desc_impl<kValidate>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
+        default: return desc_impl<kStamp>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
+    }
+}
+
+hipError_t run_gen_pages(uint8_t* pages, uint64_t P, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = grid_for(n, 1, 16);
+    hipLaunchKernelGGL(k_gen_pages, dim3(grid), dim3(kBlock), 0, s, reinterpret_cast<uint64_t*>(pages), P / 8, n, seed,
+                       first);
+    return hipGetLastError();
+}
+
+hipError_t run_gen_desc(uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n, uint64_t seed,
+                        uint64_t first, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = grid_for(n, 1, 16);
+    hipLaunchKernelGGL(k_gen_desc, dim3(grid), dim3(kBlock), 0, s, base, off, len, n, seed, first);
+    return hipGetLastError();
+}
+
+hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint64_t byte_off, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t count = (n + every - 1) / every;
+    const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_flip_byte, dim3(grid), dim3(kBlock), 0, s, pages, P, n, every, byte_off);
+    return hipGetLastError();
+}
+
+hipError_t run_read_ceiling(const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
+    switch (P) {
+#define CASE(SZ) \
+    case SZ: hipLaunchKernelGGL((k_read_ceiling<SZ>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); break;
+        CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
+#undef CASE
+        default: return hipErrorNotSupported;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace pcs

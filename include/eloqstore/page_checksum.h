@@ -1,0 +1,52 @@
+// page_checksum.h — C++ drop-in for EloqStore's page checksum call surface,
+// backed by the MI355X kernels behind include/eloqstore_pcs.h.
+//
+// Reference surface (namespace eloqstore, include/storage/page.h:11,25-26):
+//     constexpr uint8_t checksum_bytes = 8;
+//     void SetChecksum(std::string_view blob);      // src/storage/page.cpp:18-23
+//     bool ValidateChecksum(std::string_view blob);  // src/storage/page.cpp:25-31
+// Same names, namespace and argument meaning: blob is one whole page,
+// blob.size() >= 8 is assumed exactly as in the reference (a shorter blob
+// never validates and SetChecksum leaves it untouched); SetChecksum writes the
+// little-endian digest into blob[0, 8) through const_cast, as page.cpp does.
+// No exceptions: a GPU failure terminates the process with a message (the
+// reference's functions cannot fail, and a silent `false` would be reported
+// by callers as KvError::Corrupted).
+//
+// Batched forms for the natural batch points of the callers
+// (IouringMgr::ReadPages, async_io_manager.cpp:353-366; FlushBatchPages,
+// write_task.cpp:155-167) — scattered pool pages of one page size.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <span>
+#include <string_view>
+
+namespace eloqstore {
+
+inline constexpr uint8_t checksum_bytes = 8;  // include/storage/page.h:11
+
+void SetChecksum(std::string_view blob);
+bool ValidateChecksum(std::string_view blob);
+
+// Hash variant for the batched forms (the reference path is always XXH3).
+enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
+
+// Validates every page; ok_out[i] = 1 if page i's stored digest matches.
+// Returns the index of the first corrupted page, or pages.size() if all match
+// (the reference loop stops at the first failure, async_io_manager.cpp:357-363;
+// the batch checks all and reports the first).  skip_verify mirrors
+// KvOptions::skip_verify_checksum (kv_options.h:41): nothing is hashed and every
+// page is reported valid.
+size_t ValidateChecksums(std::span<const char* const> pages, size_t page_size, uint8_t* ok_out,
+                         PageHash hash = PageHash::XXH3_64, bool skip_verify = false);
+
+// Stamps every page in place (batched SetChecksum).
+void SetChecksums(std::span<char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
+
+// Digests without touching the pages.
+void PageDigests(std::span<const char* const> pages, size_t page_size, uint64_t* digests_out,
+                 PageHash hash = PageHash::XXH3_64);
+
+}  // namespace eloqstore

@@ -1,0 +1,145 @@
+/*
+ * eloqstore_pcs.h — C ABI of the MI355X page-checksum engine (libeloqstore_pcs.so).
+ *
+ * The drop-in boundary for EloqStore's per-page checksum path.  Every entry
+ * point takes plain pointers and sizes; no C++ or torch types cross it.  The
+ * reference has no batched or device API: these functions replace the bodies
+ * of
+ *     void eloqstore::SetChecksum(std::string_view)      src/storage/page.cpp:18-23
+ *     bool eloqstore::ValidateChecksum(std::string_view)  src/storage/page.cpp:25-31
+ * (declared include/storage/page.h:25-26) at the batch points of their callers:
+ *     IouringMgr::ReadPages validate loop        src/async_io_manager.cpp:353-366 (<=128 pages)
+ *     IouringMgr::ReadPage validate              src/async_io_manager.cpp:239-244
+ *     WriteTask::WritePage SetChecksum x3         src/tasks/write_task.cpp:58-79  (batched at
+ *                                                 FlushBatchPages :155-167, <=256 pages)
+ *     page_checksum_tool                         tools/page_checksum_tool.cpp:104-105
+ * and the hash primitive they call, XXH3_64bits (external/xxhash.h:6185) /
+ * XXH64 (external/xxhash.h:3678).
+ *
+ * Page convention (include/storage/page.h:11, include/coding.h:64-77,126-139):
+ * digest = XXH3_64bits(page + 8, page_size - 8) (seed 0, default secret),
+ * stored little-endian in page bytes [0, 8).  algo = PCS_XXH64 uses
+ * XXH64(page + 8, page_size - 8, 0) with the same layout (BASELINE config 3).
+ *
+ * Conventions
+ *  - Return value: PCS_OK (0) or a negative pcs_status.  pcs_last_error()
+ *    gives a thread-local message for the last failure on the calling thread.
+ *  - *_dev functions take caller-owned DEVICE pointers on the current HIP
+ *    device and enqueue work on `stream` (0 = legacy default stream); they do
+ *    not synchronise.  Results are valid after the stream is synchronised.
+ *  - Validation never fails on a mismatch: mismatches are reported through
+ *    d_ok[i] = 0 and *d_first_bad = smallest failing index (UINT64_MAX when all
+ *    pages match).  d_first_bad may be NULL.  The caller maps a mismatch to
+ *    KvError::Corrupted exactly as async_io_manager.cpp:243/362 does.
+ *  - Thread-safety: reentrant; use one stream per host thread per device.
+ *    The only global state is the immutable secret in device constant memory
+ *    and a per-device CU-count cache.
+ *  - The library has no CPU fallback: without a usable GPU every compute entry
+ *    point returns PCS_ERR_NO_DEVICE.
+ */
+#ifndef ELOQSTORE_PCS_H
+#define ELOQSTORE_PCS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* hipStream_t, kept opaque so that callers need no HIP headers. */
+typedef struct ihipStream_t *pcs_stream_t;
+
+enum pcs_status {
+    PCS_OK = 0,
+    PCS_ERR_INVALID = -1,     /* bad argument (null pointer, page_size < 8, ...) */
+    PCS_ERR_NO_DEVICE = -2,   /* no usable GPU / HIP runtime failure at init */
+    PCS_ERR_HIP = -3,         /* a HIP call or kernel launch failed */
+    PCS_ERR_NOMEM = -4,       /* device or pinned-host allocation failed */
+};
+
+enum pcs_algo {
+    PCS_XXH3_64 = 0, /* XXH3_64bits, seed 0 — the reference's page checksum */
+    PCS_XXH64 = 1,   /* XXH64, seed 0 */
+};
+
+/* ---- library / device ---------------------------------------------------- */
+const char *pcs_version(void);
+const char *pcs_last_error(void);
+int pcs_device_count(int *count);
+/* Select the HIP device for subsequent calls on this host thread. */
+int pcs_set_device(int device);
+int pcs_synchronize(pcs_stream_t stream);
+
+/* ---- device-resident, fixed page size (pages contiguous, stride page_size) --
+ * Fast paths: XXH3 needs a 16-byte-aligned base and page_size % 256 == 0
+ * (every legal EloqStore data_page_size of 1-32 KiB and 64 KiB chunks);
+ * XXH64 needs an 8-byte-aligned base, page_size % 8 == 0 and page_size >= 40.
+ * Any other shape is still computed exactly (generic kernel), only slower. */
+
+/* d_digests[i] = digest of page i over [8, page_size). */
+int pcs_pages_digest_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages, int algo,
+                         uint64_t *d_digests, pcs_stream_t stream);
+/* d_ok[i] = (stored LE u64 at page i [0,8)) == digest; batched ValidateChecksum. */
+int pcs_pages_validate_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages, int algo,
+                           uint8_t *d_ok, uint64_t *d_first_bad, pcs_stream_t stream);
+/* In place: page i bytes [0,8) = digest (LE); batched SetChecksum. */
+int pcs_pages_stamp_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, int algo,
+                        pcs_stream_t stream);
+
+/* ---- device-resident descriptor batches (mixed page sizes) ----------------
+ * Page i occupies [d_base + d_off[i], d_base + d_off[i] + d_len[i]).  Pages
+ * shorter than 8 bytes never validate (ok = 0) and digest to 0. */
+int pcs_desc_digest_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                        uint64_t n, int algo, uint64_t *d_digests, pcs_stream_t stream);
+int pcs_desc_validate_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                          uint64_t n, int algo, uint8_t *d_ok, uint64_t *d_first_bad,
+                          pcs_stream_t stream);
+int pcs_desc_stamp_dev(void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t n,
+                       int algo, pcs_stream_t stream);
+
+/* ---- raw ranges (no page header): the hash primitive itself ---------------
+ * d_out[i] = XXH3_64bits(range i)  (external/xxhash.h:6185), any length, or
+ * XXH64(range i, seed)             (external/xxhash.h:3678). */
+int pcs_xxh3_64_ranges_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                           uint64_t n, uint64_t *d_out, pcs_stream_t stream);
+int pcs_xxh64_ranges_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                         uint64_t n, uint64_t seed, uint64_t *d_out, pcs_stream_t stream);
+
+/* ---- host-memory batches (scattered pool pages, synchronous) --------------
+ * The shape of IouringMgr::ReadPages / FlushBatchPages: an array of page
+ * pointers into the caller's page pool (page.cpp:95-120).  Pages are gathered
+ * into pinned staging, hashed on the current device and results copied back;
+ * the call returns when done.  Safe to call concurrently from several host
+ * threads (each thread owns its staging and stream). */
+int pcs_pages_validate_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
+                            int algo, uint8_t *ok, uint64_t *first_bad);
+int pcs_pages_stamp_host(void *const *pages, uint64_t page_size, uint64_t n_pages, int algo);
+int pcs_pages_digest_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
+                          int algo, uint64_t *digests);
+
+/* ---- sharding ------------------------------------------------------------
+ * Contiguous page range [begin, end) of rank `rank` of `world` for n pages:
+ * begin = floor(rank * n / world).  Pages are independent, so G GPUs hash G
+ * disjoint ranges with no collective. */
+int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *end);
+
+/* ---- workload tooling (benchmarks, tests, scrub drills) -------------------
+ * Synthetic pages: word w of page p = splitmix64((seed ^ p) + (w+1) *
+ * 0x9E3779B97F4A7C15), p = first_page_index + i. */
+int pcs_gen_pages_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, uint64_t seed,
+                      uint64_t first_page_index, pcs_stream_t stream);
+int pcs_gen_desc_dev(void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t n,
+                     uint64_t seed, uint64_t first_page_index, pcs_stream_t stream);
+/* XOR 0xFF into byte `byte_offset` of every `every`-th page (pages 0, every, ...). */
+int pcs_flip_byte_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, uint64_t every,
+                      uint64_t byte_offset, pcs_stream_t stream);
+/* Streaming-read ceiling: same load pattern as the XXH3 page kernel with the
+ * hash replaced by an xor/add fold (page_size a power of two, 256..65536). */
+int pcs_read_ceiling_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages,
+                         uint64_t *d_out, pcs_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ELOQSTORE_PCS_H */

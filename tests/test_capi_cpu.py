@@ -1,0 +1,108 @@
+"""CPU-side checks of the native boundary (no GPU needed, no compute calls).
+
+- libeloqstore_pcs.so loads and exports every pcs_* symbol include/eloqstore_pcs.h
+  declares, plus the C++ drop-in symbols of include/eloqstore/page_checksum.h;
+- without a GPU every compute entry point fails loudly (PCS_ERR_NO_DEVICE),
+  never silently falling back to a CPU path;
+- argument validation and the pure host logic (shard ranges);
+- the CLI's usage / IO error contract (tools/page_checksum_tool.cpp:47-99).
+"""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import eloqstore_amd as pcs
+
+HAVE_GPU = pcs.device_count() > 0
+
+
+def test_library_exports_every_header_symbol():
+    funcs = pcs.header_functions()
+    assert len(funcs) >= 20
+    so = pcs.lib()
+    for f in funcs:
+        assert hasattr(so, f), f
+    # and the binding covers exactly the header
+    assert set(funcs) == set(pcs._SIGS)
+
+
+def test_cpp_dropin_symbols_exported():
+    out = subprocess.run(["nm", "-D", "-C", "--defined-only", pcs.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    for sym in ("eloqstore::SetChecksum(std::basic_string_view<char, std::char_traits<char> >)",
+                "eloqstore::ValidateChecksum(std::basic_string_view<char, std::char_traits<char> >)",
+                "eloqstore::ValidateChecksums(", "eloqstore::SetChecksums(", "eloqstore::PageDigests("):
+        assert sym in out, sym
+
+
+def test_version_string():
+    assert "gfx950" in pcs.version()
+
+
+@pytest.mark.skipif(HAVE_GPU, reason="checks the no-GPU failure path")
+def test_no_gpu_fails_loudly():
+    so = pcs.lib()
+    rc = so.pcs_pages_digest_dev(0, 4096, 1, 0, 0, 0)
+    assert rc == pcs.PCS_ERR_NO_DEVICE
+    assert b"no usable HIP device" in so.pcs_last_error()
+    for fn, args in (("pcs_pages_validate_dev", (0, 4096, 1, 0, 0, 0, 0)),
+                     ("pcs_pages_stamp_dev", (0, 4096, 1, 0, 0)),
+                     ("pcs_desc_digest_dev", (0, 0, 0, 1, 0, 0, 0)),
+                     ("pcs_xxh3_64_ranges_dev", (0, 0, 0, 1, 0, 0)),
+                     ("pcs_gen_pages_dev", (0, 4096, 1, 0, 0, 0))):
+        assert getattr(so, fn)(*args) == pcs.PCS_ERR_NO_DEVICE, fn
+    with pytest.raises(pcs.PcsError):
+        pcs.validate_checksum(bytearray(4096))
+
+
+def test_shard_range_partitions_exactly():
+    for n in (0, 1, 7, 1 << 20, (1 << 26) + 3):
+        for world in (1, 2, 3, 4, 8):
+            spans = [pcs.shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (b0, e0), (b1, e1) in zip(spans, spans[1:]):
+                assert e0 == b1
+            sizes = [e - b for b, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_range_rejects_bad_rank():
+    b, e = ctypes.c_uint64(), ctypes.c_uint64()
+    assert pcs.lib().pcs_shard_range(10, 2, 2, ctypes.byref(b), ctypes.byref(e)) == pcs.PCS_ERR_INVALID
+    assert pcs.lib().pcs_shard_range(10, 0, 0, ctypes.byref(b), ctypes.byref(e)) == pcs.PCS_ERR_INVALID
+
+
+def run_tool(*args):
+    return subprocess.run([pcs.TOOL_PATH, *args], capture_output=True, text=True)
+
+
+def test_cli_usage_errors(tmp_path):
+    assert os.access(pcs.TOOL_PATH, os.X_OK)
+    r = run_tool()
+    assert r.returncode == 1 and "Usage:" in r.stderr
+    r = run_tool("a", "b", "c", "d")
+    assert r.returncode == 1 and "Usage:" in r.stderr
+    f = tmp_path / "f.bin"
+    f.write_bytes(b"\0" * 8192)
+    for bad in ("x12", "12x", "", "0x"):
+        r = run_tool(str(f), bad)
+        assert r.returncode == 1 and "Invalid offset" in r.stderr, bad
+    r = run_tool(str(f), "0", "0")
+    assert r.returncode == 1 and "Invalid page size: 0" in r.stderr
+    r = run_tool(str(f), "4097")
+    assert r.returncode == 1 and "Requested range [4097, 8193) exceeds file size 8192" in r.stderr
+    r = run_tool(str(f), "0x1001", "0x1000")
+    assert r.returncode == 1 and "Requested range [4097, 8193)" in r.stderr
+    r = run_tool(str(tmp_path / "missing.bin"), "0")
+    assert r.returncode == 1 and "Failed to open" in r.stderr
+
+
+@pytest.mark.skipif(HAVE_GPU, reason="checks the no-GPU failure path")
+def test_cli_without_gpu_fails_loudly(tmp_path):
+    f = tmp_path / "f.bin"
+    f.write_bytes(b"\0" * 8192)
+    r = run_tool(str(f), "010")  # octal 8, as std::stoull(base 0) parses it
+    assert r.returncode not in (0, 2)
+    assert "no usable HIP device" in r.stderr
