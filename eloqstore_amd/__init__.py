@@ -57,10 +57,13 @@ _SIGS = {
     "pcs_gen_desc_dev": [_vp, _vp, _vp, _u64, _u64, _u64, _vp],
     "pcs_flip_byte_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
     "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
+    "pcs_set_tuning": [_i32, ctypes.c_int64],
+    "pcs_get_tuning": [_i32],
     "pcs_version": [],
     "pcs_last_error": [],
 }
 _STR = {"pcs_version", "pcs_last_error"}
+_I64 = {"pcs_get_tuning"}
 
 
 class PcsError(RuntimeError):
@@ -83,7 +86,7 @@ def lib() -> ctypes.CDLL:
         for name, args in _SIGS.items():
             f = getattr(so, name)
             f.argtypes = args
-            f.restype = ctypes.c_char_p if name in _STR else ctypes.c_int
+            f.restype = ctypes.c_char_p if name in _STR else ctypes.c_int64 if name in _I64 else ctypes.c_int
         _lib = so
     return _lib
 
@@ -118,6 +121,19 @@ def _stream(stream) -> int:
     if isinstance(stream, int):
         return stream
     return stream.cuda_stream
+
+
+TUNE_XXH3_BLOCKS_PER_CU = 1
+TUNE_XXH64_BLOCKS_PER_CU = 2
+TUNE_NT_LOADS = 3
+
+
+def set_tuning(key: int, value: int) -> None:
+    _call("pcs_set_tuning", key, value)
+
+
+def get_tuning(key: int) -> int:
+    return int(lib().pcs_get_tuning(key))
 
 
 def version() -> str:

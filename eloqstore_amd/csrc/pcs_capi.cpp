@@ -340,6 +340,13 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t* begin, uint64_t* 
     return PCS_OK;
 }
 
+int pcs_set_tuning(int key, int64_t value) {
+    if (pcs::set_tuning(key, value)) return fail(PCS_ERR_INVALID, "unknown tuning key or negative value");
+    return PCS_OK;
+}
+
+int64_t pcs_get_tuning(int key) { return pcs::get_tuning(key); }
+
 int pcs_gen_pages_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t seed, uint64_t first_page_index,
                       pcs_stream_t stream) {
     if (int rc = require_device()) return rc;

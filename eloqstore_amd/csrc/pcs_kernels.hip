@@ -24,6 +24,8 @@
 #include "xxh_device.h"
 #include "eloqstore_pcs_internal.h"
 
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 
 namespace pcs {
@@ -51,6 +53,19 @@ __constant__ KeyTables c_keys = make_tables();
 __constant__ uint64_t c_init_acc[8] = {kP32_3, kP64_1, kP64_2, kP64_3, kP64_4, kP32_2, kP64_5, kP32_1};
 
 enum Mode : int { kDigest = 0, kValidate = 1, kStamp = 2 };
+
+// Native 16-byte vector (global_load_dwordx4).  NT selects the non-temporal
+// cache policy: every page byte is read exactly once, and the nt stream
+// measured +15 % over default-policy loads on this layout (tools/lab/read_lab.hip,
+// profiles/r01_read_lab.txt).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ __forceinline__ uint64_t lo64(u32x4 v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint64_t hi64(u32x4 v) { return ((uint64_t)v.w << 32) | v.z; }
 
 // Per-page output for every kernel: digest array, verdict array + first bad
 // index, or the digest stamped little-endian into page bytes [0, 8).
@@ -85,7 +100,8 @@ __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_
 // The one word with jb = -1 (lane 0, chunk 0, e = 0) is page word 128b: it
 // belongs to the PREVIOUS block (or is the stored digest for b = 0).  Lane 0
 // instead takes page word 128(b+1) ("carry"), the block's own last input word
-// (stripe 15, lane 7, key 22), read by a separate 8-byte load.
+// (stripe 15, lane 7, key 22) — the low half of lane 0's chunk 0 of block b+1,
+// which lane 0 loads for that block anyway.
 struct Xxh3Lane {
     uint64_t k[4][2];     // accumulate keys, chunk c, half e
     uint64_t kl0, kl1;    // last-stripe keys (used by lanes 12..15)
@@ -124,15 +140,15 @@ __device__ __forceinline__ Xxh3Lane make_xxh3_lane(int g) {
 // the final chunk) keyed with secret + 121, and page words P/8-7 .. P/8-1
 // excluded from the ordinary stripes (xxhash.h:6005-6016).
 template <bool FINAL>
-__device__ __forceinline__ void xxh3_block_terms(const Xxh3Lane& L, const uint4 (&d)[4], uint64_t carry,
+__device__ __forceinline__ void xxh3_block_terms(const Xxh3Lane& L, const u32x4 (&d)[4], uint64_t carry,
                                                  int nchunks, uint64_t& Te, uint64_t& To) {
     uint64_t Ue = 0, Uo = 0, Ve = 0, Vo = 0;
     const int g = L.g;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         if (FINAL && c >= nchunks) break;
-        uint64_t w0 = ((uint64_t)d[c].y << 32) | d[c].x;
-        const uint64_t w1 = ((uint64_t)d[c].w << 32) | d[c].z;
+        uint64_t w0 = lo64(d[c]);
+        const uint64_t w1 = hi64(d[c]);
         bool use0 = true, use1 = true;
         if (c == 0) {
             if (FINAL) use0 = (g != 0);
@@ -170,37 +186,41 @@ __device__ __forceinline__ uint64_t xxh3_merge(const Xxh3Lane& L, uint64_t Ae, u
 
 // Whole page, compile-time page size P (P % 256 == 0, P >= 256).  Blocks are
 // loaded in batches of up to 4 (4 KiB per page, 16 KiB per wave in flight)
-// before any of them is folded, so a 4 KiB page is one batch.
-template <int P>
+// before any of them is folded, so a 4 KiB page is one batch.  The carry word
+// of block b (page word 128(b+1)) is lane 0's low half of chunk 0 of block
+// b+1, which lane 0 loads anyway: each batch also fetches chunk 0 of the
+// following block and hands it on, so no byte is loaded twice.
+template <int P, bool NT>
 __device__ __forceinline__ uint64_t xxh3_page_fixed(const uint8_t* __restrict__ page, const Xxh3Lane& L,
                                                     uint64_t& stored) {
     constexpr int NB = (P - 9) / 1024;   // full blocks (xxhash.h:5996)
     constexpr int R = P / 256 - 4 * NB;  // chunks in the final block, 1..4
     constexpr int TB = NB + 1;
-    const uint4* base = reinterpret_cast<const uint4*>(page) + L.g;
+    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
     uint64_t Ae = L.init_e, Ao = L.init_o;
+    u32x4 head = ld16<NT>(base);  // chunk 0 of the next block to fold
+    stored = lo64(head);
 #pragma unroll
     for (int b0 = 0; b0 < TB; b0 += 4) {
-        uint4 d[4][4];
-        uint64_t carry[4];
+        constexpr int kMaxBatch = 4;
+        u32x4 d[kMaxBatch + 1][4];
+        d[0][0] = head;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i <= kMaxBatch; ++i) {
             const int b = b0 + i;
             if (b >= TB) break;
-            const int nc = (b == NB) ? R : 4;
+            const int nc = (i == kMaxBatch) ? 1 : (b == NB) ? R : 4;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                if (c < nc) d[i][c] = base[b * 64 + c * 16];
-            if (b < NB) carry[i] = *reinterpret_cast<const uint64_t*>(page + (b + 1) * 1024);
+                if (c < nc && !(i == 0 && c == 0)) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
         }
-        if (b0 == 0) stored = ((uint64_t)d[0][0].y << 32) | d[0][0].x;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kMaxBatch; ++i) {
             const int b = b0 + i;
             if (b >= TB) break;
             uint64_t Te, To;
             if (b < NB) {
-                xxh3_block_terms<false>(L, d[i], carry[i], 4, Te, To);
+                xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
                 Ae = xxh3_scramble(Ae + Te, L.ks_e);
                 Ao = xxh3_scramble(Ao + To, L.ks_o);
             } else {
@@ -209,32 +229,36 @@ __device__ __forceinline__ uint64_t xxh3_page_fixed(const uint8_t* __restrict__ 
                 Ao += To;
             }
         }
+        if (b0 + kMaxBatch < TB) head = d[kMaxBatch][0];
     }
     return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
 }
 
-// Run-time page size (P % 256 == 0, P >= 256): one block per step.
+// Run-time page size (P % 256 == 0, P >= 256): one block per step, chunk 0 of
+// the next block prefetched with the current one (it supplies the carry).
+template <bool NT>
 __device__ __forceinline__ uint64_t xxh3_page_rt(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
                                                  uint64_t& stored) {
     const int NB = (int)((P - 9) / 1024);
     const int R = (int)(P / 256) - 4 * NB;
-    const uint4* base = reinterpret_cast<const uint4*>(page) + L.g;
+    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
     uint64_t Ae = L.init_e, Ao = L.init_o;
-    stored = *reinterpret_cast<const uint64_t*>(page);
+    u32x4 d[4];
+    d[0] = ld16<NT>(base);
+    stored = lo64(d[0]);
     for (int b = 0; b < NB; ++b) {
-        uint4 d[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) d[c] = base[b * 64 + c * 16];
-        const uint64_t carry = *reinterpret_cast<const uint64_t*>(page + (size_t)(b + 1) * 1024);
+        for (int c = 1; c < 4; ++c) d[c] = ld16<NT>(base + b * 64 + c * 16);
+        const u32x4 next0 = ld16<NT>(base + (b + 1) * 64);
         uint64_t Te, To;
-        xxh3_block_terms<false>(L, d, carry, 4, Te, To);
+        xxh3_block_terms<false>(L, d, lo64(next0), 4, Te, To);
         Ae = xxh3_scramble(Ae + Te, L.ks_e);
         Ao = xxh3_scramble(Ao + To, L.ks_o);
+        d[0] = next0;
     }
-    uint4 d[4] = {};
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-        if (c < R) d[c] = base[NB * 64 + c * 16];
+    for (int c = 1; c < 4; ++c)
+        if (c < R) d[c] = ld16<NT>(base + NB * 64 + c * 16);
     uint64_t Te, To;
     xxh3_block_terms<true>(L, d, 0, R, Te, To);
     return xxh3_merge(L, Ae + Te, Ao + To, (uint64_t)(P - 8));
@@ -244,7 +268,7 @@ __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
     return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
 }
 
-template <int P, int MODE>
+template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                    unsigned long long* first_bad) {
@@ -253,13 +277,13 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
     for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
-        const uint64_t h = xxh3_page_fixed<P>(page, L, stored);
+        const uint64_t h = xxh3_page_fixed<P, NT>(page, L, stored);
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
 
 // Fixed stride, run-time page size.
-template <int MODE>
+template <int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                     uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                     unsigned long long* first_bad) {
@@ -268,14 +292,14 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
     for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
-        const uint64_t h = xxh3_page_rt(page, P, L, stored);
+        const uint64_t h = xxh3_page_rt<NT>(page, P, L, stored);
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
 
 // Descriptor batch (mixed sizes).  Pages that miss the fast-path shape are
 // left to k_generic_desc.
-template <int MODE>
+template <int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
@@ -288,7 +312,7 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
         if (!xxh3_fast_ok(o, P)) continue;
         const uint8_t* page = base + o;
         uint64_t stored = 0;
-        const uint64_t h = xxh3_page_rt(page, P, L, stored);
+        const uint64_t h = xxh3_page_rt<NT>(page, P, L, stored);
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
@@ -590,17 +614,17 @@ __global__ void k_flip_byte(uint8_t* pages, uint64_t P, uint64_t n, uint64_t eve
 
 // Same access pattern and output as k_xxh3_fixed<P, kDigest> minus the hash:
 // the achievable HBM read rate for this layout (roofline "measured ceiling").
-template <int P>
+template <int P, bool NT>
 __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
                                                      uint64_t* __restrict__ out) {
     const int g = threadIdx.x & 15;
     const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
     for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
-        const uint4* base = reinterpret_cast<const uint4*>(pages + pg * (uint64_t)P) + g;
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P) + g;
         uint32_t x = 0, y = 0, z = 0, w = 0;
 #pragma unroll
         for (int c = 0; c < P / 256; ++c) {
-            const uint4 v = base[c * 16];
+            const u32x4 v = ld16<NT>(base + c * 16);
             x ^= v.x; y += v.y; z ^= v.z; w += v.w;
         }
         uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + w);
@@ -641,25 +665,56 @@ unsigned grid_for(uint64_t units, unsigned units_per_block, unsigned blocks_per_
 }
 
 constexpr unsigned kBlock = 256;
-constexpr unsigned kBlocksPerCu = 8;
+constexpr unsigned kBlocksPerCu = 8;  // grid-stride cap for the auxiliary kernels
 
-template <int MODE>
-hipError_t launch_xxh3_fixed(int P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
+bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) == 0; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// tuning knobs (pcs_set_tuning): read at every launch
+// ---------------------------------------------------------------------------
+namespace {
+std::atomic<int64_t> g_tune[8] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*nt*/ 1, 0, 0, 0, 0};
+}
+int set_tuning(int key, int64_t value) {
+    if (key <= 0 || key >= 8 || value < 0) return -1;
+    g_tune[key].store(value, std::memory_order_relaxed);
+    return 0;
+}
+int64_t get_tuning(int key) { return (key <= 0 || key >= 8) ? -1 : g_tune[key].load(std::memory_order_relaxed); }
+
+namespace {
+// Page kernels: the knob caps the grid at that many 256-thread blocks per CU
+// (grid-stride loop beyond); 0 = auto.  Auto launches one block per 16 (XXH3)
+// / 64 (XXH64) pages for pages up to 16 KiB and caps at 8 blocks per CU for
+// larger pages (measured, profiles/r01_kernel_lab.txt).
+unsigned page_grid(uint64_t n, unsigned pages_per_block, int key, uint64_t page_size = 0) {
+    int64_t bpc = g_tune[key].load(std::memory_order_relaxed);
+    if (bpc == 0) bpc = page_size > 16384 ? 8 : (int64_t)1 << 30;
+    const uint64_t need = (n + pages_per_block - 1) / pages_per_block;
+    const uint64_t cap = std::min<uint64_t>((uint64_t)cu_count() * (uint64_t)bpc, 0x7FFFFFFFull);
+    return (unsigned)(need < cap ? (need ? need : 1) : cap);
+}
+bool use_nt() { return g_tune[3].load(std::memory_order_relaxed) != 0; }
+
+template <int MODE, bool NT>
+hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
                              unsigned long long* fb, hipStream_t s) {
-    const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
+    const unsigned grid = page_grid(n, kBlock / 16, 1, P);
     switch (P) {
-#define CASE(SZ) \
-    case SZ: hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb); break;
+#define CASE(SZ)                                                                                             \
+    case SZ:                                                                                                 \
+        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb); \
+        break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
         default:
-            hipLaunchKernelGGL((k_xxh3_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok,
-                               fb);
+            hipLaunchKernelGGL((k_xxh3_stride<MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out,
+                               ok, fb);
     }
     return hipGetLastError();
 }
-
-bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) == 0; }
 
 }  // namespace
 
@@ -671,13 +726,11 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
     const bool aligned16 = ((uintptr_t)pages % 16) == 0;
     const bool aligned8 = ((uintptr_t)pages % 8) == 0;
     if (algo == 0 && aligned16 && P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull) {
-        if (is_pow2_page(P)) return launch_xxh3_fixed<MODE>((int)P, pages, n, out, ok, fb, s);
-        const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
-        hipLaunchKernelGGL((k_xxh3_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
-        return hipGetLastError();
+        return use_nt() ? launch_xxh3_pages<MODE, true>(P, pages, n, out, ok, fb, s)
+                        : launch_xxh3_pages<MODE, false>(P, pages, n, out, ok, fb, s);
     }
     if (algo == 1 && aligned8 && P % 8 == 0 && P >= 40 && P <= 0xFFFFFFFFull) {
-        const unsigned grid = grid_for(n, kBlock / 4, kBlocksPerCu);
+        const unsigned grid = page_grid(n, kBlock / 4, 2, P);
         hipLaunchKernelGGL((k_xxh64_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
         return hipGetLastError();
     }
@@ -701,10 +754,13 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
     if (skip == 8 && seed == 0) {
         // fast kernels for conforming pages, generic lanes for the rest
         if (algo == 0) {
-            const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
-            hipLaunchKernelGGL((k_xxh3_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+            const unsigned grid = page_grid(n, kBlock / 16, 1);
+            if (use_nt())
+                hipLaunchKernelGGL((k_xxh3_desc<MODE, true>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+            else
+                hipLaunchKernelGGL((k_xxh3_desc<MODE, false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
         } else {
-            const unsigned grid = grid_for(n, kBlock / 4, kBlocksPerCu);
+            const unsigned grid = page_grid(n, kBlock / 4, 2);
             hipLaunchKernelGGL((k_xxh64_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
         }
         hipError_t e = hipGetLastError();
@@ -755,10 +811,14 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 
 hipError_t run_read_ceiling(const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const unsigned grid = grid_for(n, kBlock / 16, kBlocksPerCu);
+    const unsigned grid = page_grid(n, kBlock / 16, 1);
+    const bool nt = use_nt();
     switch (P) {
-#define CASE(SZ) \
-    case SZ: hipLaunchKernelGGL((k_read_ceiling<SZ>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); break;
+#define CASE(SZ)                                                                                            \
+    case SZ:                                                                                                \
+        if (nt) hipLaunchKernelGGL((k_read_ceiling<SZ, true>), dim3(grid), dim3(kBlock), 0, s, pages, n, out);  \
+        else hipLaunchKernelGGL((k_read_ceiling<SZ, false>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); \
+        break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
         default: return hipErrorNotSupported;

@@ -124,6 +124,23 @@ int pcs_pages_digest_host(const void *const *pages, uint64_t page_size, uint64_t
  * disjoint ranges with no collective. */
 int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *end);
 
+/* ---- tuning -------------------------------------------------------------
+ * Process-wide launch knobs, read at every launch (defaults in brackets):
+ *   PCS_TUNE_XXH3_BLOCKS_PER_CU   [0] grid cap in 256-thread blocks per CU for
+ *                                     the XXH3 page kernels (grid-stride loop
+ *                                     beyond it); 0 = auto: one block per 16
+ *                                     pages up to 16 KiB pages, 8 per CU above
+ *   PCS_TUNE_XXH64_BLOCKS_PER_CU  [0] same for XXH64 (one block per 64 pages)
+ *   PCS_TUNE_NT_LOADS             [1] non-temporal page loads (1) or default
+ *                                     cache policy (0) */
+enum pcs_tune_key {
+    PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
+    PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
+    PCS_TUNE_NT_LOADS = 3,
+};
+int pcs_set_tuning(int key, int64_t value);
+int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
+
 /* ---- workload tooling (benchmarks, tests, scrub drills) -------------------
  * Synthetic pages: word w of page p = splitmix64((seed ^ p) + (w+1) *
  * 0x9E3779B97F4A7C15), p = first_page_index + i. */

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""kernel_lab.py — interleaved A/B of the product kernels under tuning knobs.
+
+Not part of the product.  Times pcs_pages_digest_dev / pcs_desc_digest_dev
+(through the C ABI) for each variant in interleaved rounds within one process
+(cdna_hip_programming.md §5.4 rule 24) and prints median / best GB/s.
+
+    python tools/lab/kernel_lab.py [--rounds 7] [--configs 2,4,3] [--algos xxh3,xxh64]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import eloqstore_amd as pcs  # noqa: E402
+from workload import mixed_layout  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--configs", default="2,4,3")
+    ap.add_argument("--algos", default="xxh3,xxh64")
+    ap.add_argument("--bpc", default="1048576,8,32")  # 1048576 = uncapped (one block per 16 pages)
+    ap.add_argument("--nt", default="0,1")
+    args = ap.parse_args()
+    dev = "cuda:0"
+    bpcs = [int(x) for x in args.bpc.split(",")]
+    nts = [int(x) for x in args.nt.split(",")]
+
+    for cfg in [int(c) for c in args.configs.split(",")]:
+        if cfg == 3:
+            n = 1 << 20
+            offs, lens, total = mixed_layout(0x5EED0003, 0, n)
+            pages = torch.empty(total, dtype=torch.uint8, device=dev)
+            d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+            d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+            pcs.gen_desc(pages, d_off, d_len, n, 0x5EED0003, 0)
+            nbytes = total
+            P = None
+        else:
+            P, n = {2: (4096, 1 << 20), 4: (65536, 1 << 18), 5: (4096, 1 << 23)}[cfg]
+            pages = torch.empty(n * P, dtype=torch.uint8, device=dev)
+            pcs.gen_pages(pages, P, n, 0x5EED0000 + cfg, 0)
+            nbytes = n * P
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        ref = {}
+        variants = []
+        for algo_name in args.algos.split(","):
+            algo = pcs.XXH3_64 if algo_name == "xxh3" else pcs.XXH64
+            key = pcs.TUNE_XXH3_BLOCKS_PER_CU if algo == 0 else pcs.TUNE_XXH64_BLOCKS_PER_CU
+            for bpc in bpcs:
+                for nt in nts:
+                    variants.append((f"{algo_name} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash"))
+        if P in (4096, 65536):
+            for nt in nts:
+                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil"))
+
+        def run(v):
+            _, algo, key, bpc, nt, kind = v
+            pcs.set_tuning(key, bpc)
+            pcs.set_tuning(pcs.TUNE_NT_LOADS, nt)
+            if kind == "ceil":
+                pcs.read_ceiling(pages, P, n, out)
+            elif P is None:
+                pcs.desc_digest(pages, d_off, d_len, n, algo, out=out)
+            else:
+                pcs.pages_digest(pages, P, n, algo, out=out)
+
+        times = {v[0]: [] for v in variants}
+        for v in variants:  # warm + parity across variants
+            run(v)
+            torch.cuda.synchronize()
+            if v[5] == "hash":
+                d = out.clone()
+                if v[1] in ref:
+                    assert torch.equal(ref[v[1]], d), f"variant {v[0]} changed the digests"
+                else:
+                    ref[v[1]] = d
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(args.rounds):
+            for v in variants:
+                ev0.record()
+                run(v)
+                ev1.record()
+                torch.cuda.synchronize()
+                times[v[0]].append(ev0.elapsed_time(ev1))
+        print(f"== config {cfg}: {n} pages, {nbytes / 2**30:.2f} GiB", flush=True)
+        for name, t in times.items():
+            t = sorted(t)
+            med = t[len(t) // 2]
+            print(f"  {name:28s} med {med:8.4f} ms  {nbytes / med / 1e6:8.1f} GB/s  best {nbytes / t[0] / 1e6:8.1f}",
+                  flush=True)
+        del pages, out
+        torch.cuda.empty_cache()
+    pcs.set_tuning(pcs.TUNE_XXH3_BLOCKS_PER_CU, 0)
+    pcs.set_tuning(pcs.TUNE_XXH64_BLOCKS_PER_CU, 0)
+    pcs.set_tuning(pcs.TUNE_NT_LOADS, 1)
+
+
+if __name__ == "__main__":
+    main()

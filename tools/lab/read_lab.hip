@@ -1,0 +1,204 @@
+// read_lab.hip — access-pattern experiments for the page-checksum kernels.
+// Not part of the product.  Times read-only variants over 1 M x 4 KiB pages
+// (4 GiB) in interleaved rounds (one process, cdna_hip_programming.md §5.4
+// rule 24) and prints the median GB/s of each.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 read_lab.hip -o read_lab
+//   ./read_lab [rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+__device__ __forceinline__ uint32_t fold(u32x4 v) { return v.x ^ (v.y * 3u) ^ v.z ^ (v.w + 7u); }
+
+// A: 16-lane group per page, 4 pages per wave (the product layout)
+template <int P, bool NT>
+__global__ __launch_bounds__(256) void k_group16(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    const int g = threadIdx.x & 15;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 16;
+    for (uint64_t pg = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * P) + g;
+        u32x4 d[P / 256];
+#pragma unroll
+        for (int c = 0; c < P / 256; ++c) d[c] = ld<NT>(base + c * 16);
+        uint32_t r = 0;
+#pragma unroll
+        for (int c = 0; c < P / 256; ++c) r += fold(d[c]);
+        if (r == 0x12345678u) out[pg] = r;  // practically never: keeps loads live
+    }
+}
+
+// B: one page per wave, 1 KiB contiguous per wave-instruction
+template <int P, bool NT>
+__global__ __launch_bounds__(256) void k_wavepage(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t pg = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; pg < n; pg += nwaves) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * P) + lane;
+        u32x4 d[P / 1024];
+#pragma unroll
+        for (int c = 0; c < P / 1024; ++c) d[c] = ld<NT>(base + c * 64);
+        uint32_t r = 0;
+#pragma unroll
+        for (int c = 0; c < P / 1024; ++c) r += fold(d[c]);
+        if (r == 0x12345678u) out[pg] = r;
+    }
+}
+
+// C: canonical linear grid-stride, U loads in flight per lane
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_linear(const uint8_t* __restrict__ buf, uint64_t nvec, uint64_t* out) {
+    const u32x4* v = reinterpret_cast<const u32x4*>(buf);
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint32_t r = 0;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (U - 1) * stride < nvec; i += U * stride) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = ld<NT>(v + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) r += fold(d[u]);
+    }
+    for (; i < nvec; i += stride) r += fold(ld<NT>(v + i));
+    if (r == 0x12345678u) out[0] = r;
+}
+
+// D: 16-lane group per page, but the 4 pages of a wave are page-interleaved so
+// that one wave-instruction reads 1 KiB contiguous: wave w owns pages
+// 4w..4w+3 and lane l reads page 4w + (c*4 + l/16)/16 ... (contiguous 1 KiB:
+// instruction i covers bytes [i*1024, i*1024+1024) of the wave's 16 KiB span)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_group16_contig(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    constexpr int P = 4096;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; w * 4 < n; w += nwaves) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + w * 4 * P) + lane;
+        u32x4 d[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d[i] = ld<NT>(base + i * 64);
+        uint32_t r = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) r += fold(d[i]);
+        if (r == 0x12345678u) out[w] = r;
+    }
+}
+
+// E: LDS-DMA (global_load_lds_dwordx4) staging of each group's page, 16 KiB
+// per wave per step, then LDS reads.  One wave per block slice.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_glds(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    constexpr int P = 4096;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4][4 * P];  // 64 KiB: 16 KiB per wave
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; w * 4 < n; w += nwaves) {
+        const uint8_t* src = pages + w * 4 * P + lane * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024), (void __attribute__((address_space(3)))*)(&lds[wv][i * 1024]), 16, 0, NT ? 2 : 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t r = 0;
+        const u32x4* l = reinterpret_cast<const u32x4*>(&lds[wv][0]) + lane;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) r += fold(l[i * 64]);
+        if (r == 0x12345678u) out[w] = r;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+struct Variant {
+    std::string name;
+    std::function<void(hipStream_t)> run;
+    std::vector<float> ms;
+};
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
+    const uint64_t P = 4096, n = 1 << 20, bytes = n * P;
+    uint8_t* pages;
+    uint64_t* out;
+    CK(hipMalloc(&pages, bytes));
+    CK(hipMalloc(&out, n * 8));
+    CK(hipMemset(pages, 0x5A, bytes));
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+
+    std::vector<Variant> vs;
+    auto add = [&](std::string name, std::function<void(hipStream_t)> f) { vs.push_back({name, f, {}}); };
+    for (int bpc : {4, 8, 16, 32}) {
+        const unsigned grid = cus * bpc;
+        add("group16 plain bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_group16<4096, false>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("group16 nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_group16<4096, true>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+    }
+    {
+        const unsigned grid = (unsigned)(n / 16);
+        add("group16 plain nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16<4096, false>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("group16 nt    nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16<4096, true>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+    }
+    for (int bpc : {8, 16}) {
+        const unsigned grid = cus * bpc;
+        add("wavepage plain bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_wavepage<4096, false>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("wavepage nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_wavepage<4096, true>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("contig16 plain bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_contig<false>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("contig16 nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_contig<true>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("linear U4 plain bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_linear<4, false>), dim3(grid), dim3(256), 0, st, pages, bytes / 16, out); });
+        add("linear U4 nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_linear<4, true>), dim3(grid), dim3(256), 0, st, pages, bytes / 16, out); });
+        add("linear U8 nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_linear<8, true>), dim3(grid), dim3(256), 0, st, pages, bytes / 16, out); });
+    }
+    for (int bpc : {2, 4}) {
+        const unsigned grid = cus * bpc;
+        add("glds plain bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_glds<false>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("glds nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_glds<true>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+    }
+
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (auto& v : vs) v.run(s);  // warm
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < rounds; ++r)
+        for (auto& v : vs) {
+            CK(hipEventRecord(a, s));
+            v.run(s);
+            CK(hipEventRecord(b, s));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.ms.push_back(ms);
+        }
+    CK(hipGetLastError());
+    std::printf("%-34s %9s %9s %9s\n", "variant", "med_ms", "GB/s", "best GB/s");
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const float med = v.ms[v.ms.size() / 2];
+        std::printf("%-34s %9.4f %9.1f %9.1f\n", v.name.c_str(), med, bytes / (med * 1e-3) / 1e9,
+                    bytes / (v.ms[0] * 1e-3) / 1e9);
+    }
+    return 0;
+}
