@@ -126,6 +126,7 @@ def _stream(stream) -> int:
 TUNE_XXH3_BLOCKS_PER_CU = 1
 TUNE_XXH64_BLOCKS_PER_CU = 2
 TUNE_NT_LOADS = 3
+TUNE_XXH64_NT_LOADS = 4
 
 
 def set_tuning(key: int, value: int) -> None:

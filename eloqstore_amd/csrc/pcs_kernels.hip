@@ -373,6 +373,12 @@ __device__ __forceinline__ uint64_t xxh64_quad_merge(uint64_t v) {
 // Page convention: XXH64 over [8, P).  Needs 8-byte aligned page, P % 8 == 0,
 // P >= 40 (so the hashed length is >= 32 and the 4-accumulator loop runs).
 constexpr int kX64Unroll = 16;
+template <bool NT>
+__device__ __forceinline__ uint64_t ld8(const uint64_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
 __device__ __forceinline__ uint64_t xxh64_page(const uint8_t* __restrict__ page, uint32_t P, int a,
                                                uint64_t& stored) {
     const uint64_t len = P - 8;
@@ -384,20 +390,111 @@ __device__ __forceinline__ uint64_t xxh64_page(const uint8_t* __restrict__ page,
     for (; s + kX64Unroll <= ns; s += kX64Unroll) {
         uint64_t x[kX64Unroll];
 #pragma unroll
-        for (int u = 0; u < kX64Unroll; ++u) x[u] = w[4 * (s + u)];
+        for (int u = 0; u < kX64Unroll; ++u) x[u] = ld8<NT>(w + 4 * (s + u));
 #pragma unroll
         for (int u = 0; u < kX64Unroll; ++u) v = xxh64_round(v, x[u]);
     }
-    for (; s < ns; ++s) v = xxh64_round(v, w[4 * s]);
+    for (; s < ns; ++s) v = xxh64_round(v, ld8<NT>(w + 4 * s));
     const uint64_t h = xxh64_quad_merge(v) + len;
     return xxh64_tail(h, page + 8 + 32 * (uint64_t)ns, len);
+}
+
+// XXH64 with full-line loads (page_size % 64 == 0, 16-byte aligned page).
+//
+// Lane q of a quad loads page bytes [64k + 16q, +16) of chunk k — page words
+// 8k + 2q (half e0) and 8k + 2q + 1 (e1) — so a wave-instruction reads sixteen
+// whole 64-byte pieces.  XXH64 stripe s covers page words 4s+1 .. 4s+4 and
+// accumulator a consumes page word 4s + a + 1.  Accumulators are placed as
+// lane q -> acc {0, 1, 3, 2}[q]; acc 3 runs one stripe behind (stripes 2k-1
+// and 2k per chunk).  Then each lane needs its own half of one word and its
+// partner's (q ^ 2) other half:
+//   lane 0 (acc 0): own e1 (stripe 2k),   partner e1 (2k+1)
+//   lane 1 (acc 1): own e0 (2k),          partner e0 (2k+1)
+//   lane 2 (acc 3): partner e0 (2k-1),    own e0 (2k)
+//   lane 3 (acc 2): partner e1 (2k),      own e1 (2k+1)
+// i.e. one DPP quad_perm [2,3,0,1] exchange of a selected half per chunk.
+// acc 3 skips stripe -1 (page word 0 is the stored digest); in the last
+// chunk accs 0-2 skip stripe 2k+1, which is the 24-byte tail (page words
+// P/8-3 .. P/8-1: lane 2 e1, lane 3 e0, lane 3 e1), consumed after the merge
+// (xxhash.h:3537-3566, 3611-3634).
+constexpr int kQuadSwap = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // quad_perm [2,3,0,1]
+
+template <bool SKIP>
+__device__ __forceinline__ void xxh64_chunk(uint64_t& v, u32x4 d, int q, bool skip_first, bool skip_second) {
+    const uint64_t e0 = lo64(d), e1 = hi64(d);
+    const bool sends_e0 = (q == 0) || (q == 3);
+    const uint64_t send = sends_e0 ? e0 : e1;
+    const uint64_t keep = sends_e0 ? e1 : e0;
+    const uint64_t recv = dpp64<kQuadSwap>(send);
+    const uint64_t first = q < 2 ? keep : recv;
+    const uint64_t second = q < 2 ? recv : keep;
+    if constexpr (SKIP) {
+        const uint64_t v1 = xxh64_round(v, first);
+        v = skip_first ? v : v1;
+        const uint64_t v2 = xxh64_round(v, second);
+        v = skip_second ? v : v2;
+    } else {
+        v = xxh64_round(xxh64_round(v, first), second);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ uint64_t xxh64_page_lines(const uint8_t* __restrict__ page, uint32_t P, int q,
+                                                     uint64_t& stored) {
+    constexpr int U = 8;  // chunks in flight per lane (128 B per lane, 8 KiB per wave)
+    const int K = (int)(P / 64);  // >= 2
+    const u32x4* base = reinterpret_cast<const u32x4*>(page) + q;
+    const int a = q == 2 ? 3 : q == 3 ? 2 : q;
+    uint64_t v = xxh64_init(a);
+    // chunk 0: acc 3 (lane 2) has no stripe -1; page word 0 is the stored digest
+    const u32x4 d0 = ld16<NT>(base);
+    stored = dpp64<quad_bcast(0)>(lo64(d0));
+    xxh64_chunk<true>(v, d0, q, q == 2, false);
+    // chunks 1 .. K-2: no skips
+    int k = 1;
+    for (; k + U <= K - 1; k += U) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = ld16<NT>(base + 4 * (k + u));
+#pragma unroll
+        for (int u = 0; u < U; ++u) xxh64_chunk<false>(v, d[u], q, false, false);
+    }
+    for (; k < K - 1; ++k) xxh64_chunk<false>(v, ld16<NT>(base + 4 * k), q, false, false);
+    // chunk K-1: stripe 2k+1 is the 24-byte tail for accs 0-2
+    const u32x4 last = ld16<NT>(base + 4 * (K - 1));
+    xxh64_chunk<true>(v, last, q, false, q != 2);
+    // merge in accumulator order: acc 0,1,2,3 live in lanes 0,1,3,2
+    const uint64_t v0 = dpp64<quad_bcast(0)>(v);
+    const uint64_t v1 = dpp64<quad_bcast(1)>(v);
+    const uint64_t v2 = dpp64<quad_bcast(3)>(v);
+    const uint64_t v3 = dpp64<quad_bcast(2)>(v);
+    uint64_t h = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
+    h = (h ^ xxh64_round(0, v0)) * kP64_1 + kP64_4;
+    h = (h ^ xxh64_round(0, v1)) * kP64_1 + kP64_4;
+    h = (h ^ xxh64_round(0, v2)) * kP64_1 + kP64_4;
+    h = (h ^ xxh64_round(0, v3)) * kP64_1 + kP64_4;
+    h += (uint64_t)(P - 8);
+    const uint64_t t0 = dpp64<quad_bcast(2)>(hi64(last));
+    const uint64_t t1 = dpp64<quad_bcast(3)>(lo64(last));
+    const uint64_t t2 = dpp64<quad_bcast(3)>(hi64(last));
+    h ^= xxh64_round(0, t0);
+    h = rotl64(h, 27) * kP64_1 + kP64_4;
+    h ^= xxh64_round(0, t1);
+    h = rotl64(h, 27) * kP64_1 + kP64_4;
+    h ^= xxh64_round(0, t2);
+    h = rotl64(h, 27) * kP64_1 + kP64_4;
+    return xxh64_avalanche(h);
+}
+
+__device__ __forceinline__ bool xxh64_lines_ok(uint64_t off, uint32_t P) {
+    return (P % 64u) == 0 && P >= 128u && (off % 16u) == 0;
 }
 
 __device__ __forceinline__ bool xxh64_fast_ok(uint64_t off, uint32_t P) {
     return (P % 8u) == 0 && P >= 40u && (off % 8u) == 0;
 }
 
-template <int MODE>
+template <int MODE, bool NT, bool LINES>
 __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                      uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                      unsigned long long* first_bad) {
@@ -406,12 +503,12 @@ __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict_
     for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; pg < n; pg += nquads) {
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
-        const uint64_t h = xxh64_page(page, P, a, stored);
+        const uint64_t h = LINES ? xxh64_page_lines<NT>(page, P, a, stored) : xxh64_page<false>(page, P, a, stored);
         if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
 
-template <int MODE>
+template <int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                    const uint32_t* __restrict__ len, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
@@ -424,7 +521,8 @@ __global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ 
         if (!xxh64_fast_ok(o, P)) continue;
         const uint8_t* page = base + o;
         uint64_t stored = 0;
-        const uint64_t h = xxh64_page(page, P, a, stored);
+        const uint64_t h = xxh64_lines_ok(o, P) ? xxh64_page_lines<NT>(page, P, a, stored)
+                                                : xxh64_page<false>(page, P, a, stored);
         if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
@@ -675,7 +773,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-std::atomic<int64_t> g_tune[8] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*nt*/ 1, 0, 0, 0, 0};
+std::atomic<int64_t> g_tune[8] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1, /*xxh64 nt*/ 0, 0, 0, 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= 8 || value < 0) return -1;
@@ -697,6 +795,7 @@ unsigned page_grid(uint64_t n, unsigned pages_per_block, int key, uint64_t page_
     return (unsigned)(need < cap ? (need ? need : 1) : cap);
 }
 bool use_nt() { return g_tune[3].load(std::memory_order_relaxed) != 0; }
+bool use_nt64() { return g_tune[4].load(std::memory_order_relaxed) != 0; }
 
 template <int MODE, bool NT>
 hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
@@ -731,7 +830,16 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
     }
     if (algo == 1 && aligned8 && P % 8 == 0 && P >= 40 && P <= 0xFFFFFFFFull) {
         const unsigned grid = page_grid(n, kBlock / 4, 2, P);
-        hipLaunchKernelGGL((k_xxh64_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
+        const bool lines = aligned16 && P % 64 == 0 && P >= 128;
+        if (lines && use_nt64())
+            hipLaunchKernelGGL((k_xxh64_stride<MODE, true, true>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
+                               n, out, ok, fb);
+        else if (lines)
+            hipLaunchKernelGGL((k_xxh64_stride<MODE, false, true>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
+                               n, out, ok, fb);
+        else
+            hipLaunchKernelGGL((k_xxh64_stride<MODE, false, false>), dim3(grid), dim3(kBlock), 0, s, pages,
+                               (uint32_t)P, n, out, ok, fb);
         return hipGetLastError();
     }
     return hipErrorNotSupported;  // caller falls back to the descriptor path
@@ -761,7 +869,10 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
                 hipLaunchKernelGGL((k_xxh3_desc<MODE, false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
-            hipLaunchKernelGGL((k_xxh64_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+            if (use_nt64())
+                hipLaunchKernelGGL((k_xxh64_desc<MODE, true>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+            else
+                hipLaunchKernelGGL((k_xxh64_desc<MODE, false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

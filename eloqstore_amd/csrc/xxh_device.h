@@ -67,7 +67,17 @@ __device__ __forceinline__ uint64_t mul32x32(uint64_t x) {
     return (uint64_t)(uint32_t)x * (uint64_t)(uint32_t)(x >> 32);
 }
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+// 64-bit rotate left by a compile-time 0 < r < 32: two v_alignbit_b32
+// (the generic shift/or form costs ~5 VALU ops per rotate).
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+    if (__builtin_constant_p(r) && r > 0 && r < 32) {
+        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+        const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+        const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+        return ((uint64_t)nhi << 32) | nlo;
+    }
+    return (x << r) | (x >> (64 - r));
+}
 
 // XXH3_avalanche (xxhash.h:4583-4589)
 __device__ __forceinline__ uint64_t xxh3_avalanche(uint64_t h) {

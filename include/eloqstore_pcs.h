@@ -131,12 +131,16 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     beyond it); 0 = auto: one block per 16
  *                                     pages up to 16 KiB pages, 8 per CU above
  *   PCS_TUNE_XXH64_BLOCKS_PER_CU  [0] same for XXH64 (one block per 64 pages)
- *   PCS_TUNE_NT_LOADS             [1] non-temporal page loads (1) or default
- *                                     cache policy (0) */
+ *   PCS_TUNE_NT_LOADS             [1] XXH3 page loads non-temporal (1) or
+ *                                     default cache policy (0)
+ *   PCS_TUNE_XXH64_NT_LOADS       [0] same for the XXH64 page kernels (their
+ *                                     64-byte-per-page pieces lose the line's
+ *                                     other half under nt: measured slower) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
     PCS_TUNE_NT_LOADS = 3,
+    PCS_TUNE_XXH64_NT_LOADS = 4,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -8,8 +8,12 @@ Not part of the product.  Times pcs_pages_digest_dev / pcs_desc_digest_dev
     python tools/lab/kernel_lab.py [--rounds 7] [--configs 2,4,3] [--algos xxh3,xxh64]
 """
 import argparse
+import ctypes
 import os
 import sys
+
+if "--system-hip" in sys.argv:  # load ROCm's own HIP runtime before torch's bundled one
+    ctypes.CDLL("/opt/rocm/lib/libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
 
 import numpy as np
 import torch
@@ -28,8 +32,11 @@ def main():
     ap.add_argument("--algos", default="xxh3,xxh64")
     ap.add_argument("--bpc", default="1048576,8,32")  # 1048576 = uncapped (one block per 16 pages)
     ap.add_argument("--nt", default="0,1")
+    ap.add_argument("--system-hip", action="store_true")
+    ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
     args = ap.parse_args()
     dev = "cuda:0"
+    print("torch", torch.__version__, "hip runtime:", [l for l in open("/proc/self/maps").read().split() if "amdhip64" in l][:1])
     bpcs = [int(x) for x in args.bpc.split(",")]
     nts = [int(x) for x in args.nt.split(",")]
 
@@ -45,7 +52,13 @@ def main():
             P = None
         else:
             P, n = {2: (4096, 1 << 20), 4: (65536, 1 << 18), 5: (4096, 1 << 23)}[cfg]
-            pages = torch.empty(n * P, dtype=torch.uint8, device=dev)
+            if args.raw_alloc:
+                hip = ctypes.CDLL("libamdhip64.so.7")
+                ptr = ctypes.c_void_p()
+                assert hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(n * P)) == 0
+                pages = ptr.value
+            else:
+                pages = torch.empty(n * P, dtype=torch.uint8, device=dev)
             pcs.gen_pages(pages, P, n, 0x5EED0000 + cfg, 0)
             nbytes = n * P
         out = torch.empty(n, dtype=torch.int64, device=dev)
@@ -64,7 +77,7 @@ def main():
         def run(v):
             _, algo, key, bpc, nt, kind = v
             pcs.set_tuning(key, bpc)
-            pcs.set_tuning(pcs.TUNE_NT_LOADS, nt)
+            pcs.set_tuning(pcs.TUNE_NT_LOADS if algo == 0 else pcs.TUNE_XXH64_NT_LOADS, nt)
             if kind == "ceil":
                 pcs.read_ceiling(pages, P, n, out)
             elif P is None:
@@ -85,6 +98,7 @@ def main():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(args.rounds):
             for v in variants:
+                torch.cuda._sleep(1_000_000)  # keep the GPU busy while the launch is enqueued
                 ev0.record()
                 run(v)
                 ev1.record()
@@ -96,11 +110,14 @@ def main():
             med = t[len(t) // 2]
             print(f"  {name:28s} med {med:8.4f} ms  {nbytes / med / 1e6:8.1f} GB/s  best {nbytes / t[0] / 1e6:8.1f}",
                   flush=True)
-        del pages, out
+        if not isinstance(pages, int):
+            del pages
+        del out
         torch.cuda.empty_cache()
     pcs.set_tuning(pcs.TUNE_XXH3_BLOCKS_PER_CU, 0)
     pcs.set_tuning(pcs.TUNE_XXH64_BLOCKS_PER_CU, 0)
     pcs.set_tuning(pcs.TUNE_NT_LOADS, 1)
+    pcs.set_tuning(pcs.TUNE_XXH64_NT_LOADS, 0)
 
 
 if __name__ == "__main__":

@@ -3,9 +3,11 @@
 // (4 GiB) in interleaved rounds (one process, cdna_hip_programming.md §5.4
 // rule 24) and prints the median GB/s of each.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++20 read_lab.hip -o read_lab
-//   ./read_lab [rounds]
+//   make -C tools/lab        (links the product library for A/B against it)
+//   ./tools/lab/read_lab [rounds] [const]
 #include <hip/hip_runtime.h>
+
+#include "eloqstore_pcs.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -130,6 +132,40 @@ __global__ __launch_bounds__(256) void k_glds(const uint8_t* __restrict__ pages,
     }
 }
 
+// F: XXH64 pattern: one quad per page, 16 pages per wave, 64 B per page per
+// wave-instruction, U chunks in flight per lane.
+template <int P, bool NT, int U>
+__global__ __launch_bounds__(256) void k_quad64(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    const int q = threadIdx.x & 3;
+    const uint64_t nq = (uint64_t)gridDim.x * 64;
+    for (uint64_t pg = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2; pg < n; pg += nq) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * P) + q;
+        uint32_t r = 0;
+        for (int k = 0; k < P / 64; k += U) {
+            u32x4 d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = ld<NT>(base + 4 * (k + u));
+#pragma unroll
+            for (int u = 0; u < U; ++u) r += fold(d[u]);
+        }
+        if (r == 0x12345678u) out[pg] = r;
+    }
+}
+
+__global__ void k_fill(uint64_t* p, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = i * 0x9E3779B97F4A7C15ull + 12345;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+__global__ void k_spin(long long cycles) {
+    const long long t0 = clock64();
+    while (clock64() - t0 < cycles) __builtin_amdgcn_s_sleep(10);
+}
+
 struct Variant {
     std::string name;
     std::function<void(hipStream_t)> run;
@@ -143,7 +179,18 @@ int main(int argc, char** argv) {
     uint64_t* out;
     CK(hipMalloc(&pages, bytes));
     CK(hipMalloc(&out, n * 8));
-    CK(hipMemset(pages, 0x5A, bytes));
+    const bool random = !(argc > 2 && std::string(argv[2]) == "const");
+    const bool gen = argc > 2 && std::string(argv[2]) == "gen";
+    if (gen) {
+        if (pcs_gen_pages_dev(pages, P, n, 0x5EED0002, 0, nullptr)) std::exit(2);
+        CK(hipDeviceSynchronize());
+    } else if (random) {
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(pages), bytes / 8);
+        CK(hipDeviceSynchronize());
+    } else {
+        CK(hipMemset(pages, 0x5A, bytes));
+    }
+    std::printf("data: %s\n", gen ? "pcs_gen_pages_dev pages" : random ? "random (splitmix64)" : "constant 0x5A");
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     hipStream_t s;
@@ -171,6 +218,16 @@ int main(int argc, char** argv) {
         add("linear U4 nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_linear<4, true>), dim3(grid), dim3(256), 0, st, pages, bytes / 16, out); });
         add("linear U8 nt    bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_linear<8, true>), dim3(grid), dim3(256), 0, st, pages, bytes / 16, out); });
     }
+    {
+        const unsigned grid = (unsigned)(n / 64);
+        add("quad64 nt U8 nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_quad64<4096, true, 8>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("quad64 plain U8 nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_quad64<4096, false, 8>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("quad64 nt U16 nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_quad64<4096, true, 16>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+        add("quad64 nt U4 nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_quad64<4096, true, 4>), dim3(grid), dim3(256), 0, st, pages, n, out); });
+    }
+    add("PRODUCT pcs_read_ceiling_dev", [=](hipStream_t st) { pcs_read_ceiling_dev(pages, 4096, n, out, (pcs_stream_t)st); });
+    add("PRODUCT pcs_pages_digest_dev xxh3", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 0, out, (pcs_stream_t)st); });
+    add("PRODUCT pcs_pages_digest_dev xxh64", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 1, out, (pcs_stream_t)st); });
     for (int bpc : {2, 4}) {
         const unsigned grid = cus * bpc;
         add("glds plain bpc=" + std::to_string(bpc), [=](hipStream_t st) { hipLaunchKernelGGL((k_glds<false>), dim3(grid), dim3(256), 0, st, pages, n, out); });
@@ -184,6 +241,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     for (int r = 0; r < rounds; ++r)
         for (auto& v : vs) {
+            hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 200000LL);  // GPU busy while we enqueue
             CK(hipEventRecord(a, s));
             v.run(s);
             CK(hipEventRecord(b, s));
