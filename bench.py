@@ -195,6 +195,34 @@ def cpu_baseline(w: Workload, target_s: float):
         {"pages": int(host.nbytes // P), "mismatches": int((want != gpu).sum())}
 
 
+def host_inclusive(w: Workload, max_pages: int = 1 << 18):
+    """Pages starting in host memory: H2D + kernel + D2H of digests, through
+    pcs_pages_digest_host.  (a) one contiguous pinned run -> direct DMA;
+    (b) pageable pages -> gather into pinned staging.  Not the headline value."""
+    if w.P is None:
+        return None
+    k = min(w.n, max_pages)
+    nbytes = k * w.P
+    pinned = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(w.pages[:nbytes])
+    pageable = pinned.numpy().copy()
+    digests = np.empty(k, dtype=np.uint64)
+    res = {"pages": k, "page_size": w.P, "bytes": nbytes}
+    for name, base in (("direct_pinned", pinned.data_ptr()), ("gather_pageable", pageable.ctypes.data)):
+        ptrs = (np.arange(k, dtype=np.uint64) * np.uint64(w.P) + np.uint64(base))
+        fn = pcs.lib().pcs_pages_digest_host
+        rc = fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)  # warm (allocates staging)
+        assert rc == 0, pcs.lib().pcs_last_error()
+        reps, t0 = 0, time.perf_counter()
+        while reps < 3 or time.perf_counter() - t0 < 2.0:
+            fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+        res[f"{name}_GiBps"] = round(nbytes / dt / GIB, 2)
+        res[f"{name}_digests_match_device"] = bool(np.array_equal(digests, w.out[:k].cpu().numpy().view(np.uint64)))
+    return res
+
+
 def committed_traffic(cfg: int, algo: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     best = None
@@ -220,6 +248,8 @@ def main():
     ap.add_argument("--pages-per-gpu", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-inclusive", action="store_true",
+                    help="also time the host-memory path (pinned direct DMA and pageable gather)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -262,6 +292,7 @@ def main():
     cpu, parity = (None, None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(w, args.cpu_seconds)
+    hostinc = host_inclusive(w) if args.host_inclusive and rank == 0 else None
 
     if rank == 0:
         achieved = w.algorithmic_bytes() / avg_launch / 1e9
@@ -304,6 +335,8 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if hostinc is not None:
+            line["host_inclusive"] = hostinc
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -117,13 +117,15 @@ struct Slot {
     uint64_t* d_dig = nullptr;
     uint8_t* h_ok = nullptr;     // pinned
     uint8_t* d_ok = nullptr;
-    size_t cap_pages_bytes = 0, cap_n = 0;
+    size_t cap_pages_bytes = 0, cap_dev_bytes = 0, cap_n = 0;
     uint64_t first = 0, count = 0;  // chunk currently in flight
     bool busy = false;
 };
 
+constexpr int kSlots = 3;  // H2D of chunk k+1 || kernel k || D2H k-1
+
 struct HostCtx {
-    Slot slot[2];
+    Slot slot[kSlots];
     ~HostCtx() {
         for (auto& s : slot) {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -146,14 +148,19 @@ int ensure_slot(Slot& s, size_t page_bytes, size_t n) {
         return hip_fail(e, "hipStreamCreate");
     if (page_bytes > s.cap_pages_bytes) {
         (void)hipHostFree(s.h_pages);
-        (void)hipFree(s.d_pages);
         s.h_pages = nullptr;
-        s.d_pages = nullptr;
         s.cap_pages_bytes = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_pages), page_bytes, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.d_pages), page_bytes) != hipSuccess)
+        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_pages), page_bytes, hipHostMallocDefault) != hipSuccess)
             return fail(PCS_ERR_NOMEM, "staging allocation failed");
         s.cap_pages_bytes = page_bytes;
+    }
+    if (page_bytes > s.cap_dev_bytes) {
+        (void)hipFree(s.d_pages);
+        s.d_pages = nullptr;
+        s.cap_dev_bytes = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&s.d_pages), page_bytes) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "staging allocation failed");
+        s.cap_dev_bytes = page_bytes;
     }
     if (n > s.cap_n) {
         (void)hipHostFree(s.h_dig);
@@ -189,8 +196,28 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     HostCtx& ctx = t_ctx[dev];
     const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, kStageBytes / P));
+    // Pages that are one contiguous, pinned (hipHostMalloc'd / hipHostRegister'ed)
+    // run are DMA'd straight from the caller's memory: no gather copy.
+    bool direct = true;
+    const uint8_t* base = static_cast<const uint8_t*>(pages[0]);
+    for (uint64_t i = 1; i < n && direct; ++i) direct = pages[i] == base + i * P;
+    if (direct) {
+        hipPointerAttribute_t attr{};
+        direct = hipPointerGetAttributes(&attr, base) == hipSuccess && attr.type == hipMemoryTypeHost;
+        (void)hipGetLastError();
+    }
     for (auto& s : ctx.slot)
-        if (int rc = ensure_slot(s, chunk * P, chunk)) return rc;
+        if (int rc = ensure_slot(s, direct ? 0 : chunk * P, chunk)) return rc;
+    if (direct)  // device page buffers are still needed per slot
+        for (auto& s : ctx.slot)
+            if (chunk * P > s.cap_dev_bytes) {
+                (void)hipFree(s.d_pages);
+                s.d_pages = nullptr;
+                s.cap_dev_bytes = 0;
+                if (hipMalloc(reinterpret_cast<void**>(&s.d_pages), chunk * P) != hipSuccess)
+                    return fail(PCS_ERR_NOMEM, "staging allocation failed");
+                s.cap_dev_bytes = chunk * P;
+            }
 
     uint64_t bad = UINT64_MAX;
     auto drain = [&](Slot& s) -> int {
@@ -215,13 +242,15 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
     int rc = PCS_OK;
     uint64_t k = 0;
     for (uint64_t first = 0; first < n && rc == PCS_OK; first += chunk, ++k) {
-        Slot& s = ctx.slot[k & 1];
+        Slot& s = ctx.slot[k % kSlots];
         if ((rc = drain(s))) break;
         const uint64_t cnt = std::min(chunk, n - first);
-        for (uint64_t i = 0; i < cnt; ++i) std::memcpy(s.h_pages + i * P, pages[first + i], P);
+        if (!direct)
+            for (uint64_t i = 0; i < cnt; ++i) std::memcpy(s.h_pages + i * P, pages[first + i], P);
         s.first = first;
         s.count = cnt;
-        e = hipMemcpyAsync(s.d_pages, s.h_pages, cnt * P, hipMemcpyHostToDevice, s.stream);
+        e = hipMemcpyAsync(s.d_pages, direct ? base + first * P : s.h_pages, cnt * P, hipMemcpyHostToDevice,
+                           s.stream);
         if (e == hipSuccess)
             e = pcs::run_pages(mode == 1 ? 1 : 0, algo, s.d_pages, P, cnt, s.d_dig, s.d_ok, nullptr, s.stream);
         if (e == hipErrorNotSupported) {

@@ -110,8 +110,11 @@ int pcs_xxh64_ranges_dev(const void *d_base, const uint64_t *d_off, const uint32
  * The shape of IouringMgr::ReadPages / FlushBatchPages: an array of page
  * pointers into the caller's page pool (page.cpp:95-120).  Pages are gathered
  * into pinned staging, hashed on the current device and results copied back;
- * the call returns when done.  Safe to call concurrently from several host
- * threads (each thread owns its staging and stream). */
+ * the call returns when done.  When the pages form one contiguous run in
+ * pinned memory (hipHostMalloc / hipHostRegister, e.g. a registered io_uring
+ * buffer ring), they are DMA'd directly with no gather copy.  32 MiB chunks
+ * flow through three slots (H2D || kernel || D2H).  Safe to call concurrently
+ * from several host threads (each thread owns its staging and streams). */
 int pcs_pages_validate_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
                             int algo, uint8_t *ok, uint64_t *first_bad);
 int pcs_pages_stamp_host(void *const *pages, uint64_t page_size, uint64_t n_pages, int algo);

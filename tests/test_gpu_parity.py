@@ -4,6 +4,7 @@ reference-generated golden vectors.  Bit-exact on every digest.
 Runs only on an MI355X (`pytest -m gpu`).  Every call goes through
 libeloqstore_pcs.so; the oracle is only the checker.
 """
+import ctypes
 import json
 import os
 import subprocess
@@ -341,3 +342,31 @@ def test_read_ceiling_runs():
     out = torch.empty(n, dtype=torch.int64, device=DEV)
     pcs.read_ceiling(buf, P, n, out)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+def test_host_direct_pinned_path(algo):
+    """Contiguous pinned pages take the direct-DMA branch of the host pipeline
+    (no gather); pageable pages of the same content take the gather branch."""
+    P, n = 4096, 20000  # > 2 staging chunks of 32 MiB
+    dev = dev_pages(P, n, 0x5EED00B0, 0)
+    pinned = torch.empty(n * P, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(dev)
+    want = oracle.pages_digest(pinned.numpy(), P, algo)
+    out = np.empty(n, dtype=np.uint64)
+    pageable = pinned.numpy().copy()  # keep a reference: the pointer must outlive the call
+    for base in (pinned.data_ptr(), pageable.ctypes.data):
+        ptrs = np.arange(n, dtype=np.uint64) * np.uint64(P) + np.uint64(base)
+        rc = pcs.lib().pcs_pages_digest_host(ptrs.ctypes.data, P, n, algo, out.ctypes.data)
+        assert rc == 0, pcs.lib().pcs_last_error()
+        assert np.array_equal(out, want)
+    # validate through the direct path, with corruption
+    pcs.pages_stamp(dev, P, n, algo)
+    pinned.copy_(dev)
+    host = pinned.numpy()
+    host[777 * P + 10] ^= 0xFF
+    ptrs = np.arange(n, dtype=np.uint64) * np.uint64(P) + np.uint64(pinned.data_ptr())
+    ok = np.empty(n, dtype=np.uint8)
+    fb = ctypes.c_uint64(0)
+    rc = pcs.lib().pcs_pages_validate_host(ptrs.ctypes.data, P, n, algo, ok.ctypes.data, ctypes.byref(fb))
+    assert rc == 0 and fb.value == 777 and int((ok == 0).sum()) == 1

@@ -1,0 +1,69 @@
+"""Multi-rank sharding on CPU (gloo, world size 2): the N>1 path of bench.py
+without a GPU.
+
+Each rank takes its page range from pcs_shard_range (the native library's
+host logic), hashes its shard with the oracle (CPU stand-in for the kernel,
+which the GPU tests cover), and the gathered digests must equal the
+single-process result.  Also exercises bench.py's barrier / max / sum helpers
+under a real process group.
+"""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N_PAGES, P, SEED = 1000, 4096, 0x5EED0005
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def worker(rank: int, world: int, port: int, out_dir: str):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import eloqstore_amd as pcs
+    import oracle
+    from workload import fill_pages
+
+    b, e = pcs.shard_range(N_PAGES, world, rank)
+    pages = fill_pages(SEED, b, e - b, P).reshape(-1)
+    dig = oracle.pages_digest(pages, P).view(np.int64)
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([e - b]))
+    maxn = int(max(s.item() for s in sizes))
+    buf = torch.zeros(maxn, dtype=torch.int64)
+    buf[: e - b] = torch.from_numpy(dig)
+    parts = [torch.zeros(maxn, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    gathered = torch.cat([parts[r][: int(sizes[r].item())] for r in range(world)])
+
+    bench.barrier(dist)
+    mx = bench.max_over_ranks(dist, float(rank + 1))
+    sm = bench.sum_over_ranks(dist, float(e - b))
+    if rank == 0:
+        np.save(os.path.join(out_dir, "gathered.npy"), gathered.numpy())
+        with open(os.path.join(out_dir, "stats.txt"), "w") as f:
+            f.write(f"{mx} {sm}\n")
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_match_single_process(tmp_path):
+    world = 2
+    mp.spawn(worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    import oracle
+    from workload import fill_pages
+
+    gathered = np.load(tmp_path / "gathered.npy").view(np.uint64)
+    single = oracle.pages_digest(fill_pages(SEED, 0, N_PAGES, P).reshape(-1), P)
+    assert np.array_equal(gathered, single)
+    mx, sm = open(tmp_path / "stats.txt").read().split()
+    assert float(mx) == world and float(sm) == N_PAGES
