@@ -256,11 +256,12 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = init_dist(world)
-    torch.cuda.set_device(local)
-    pcs.lib()
-    if pcs.lib().pcs_set_device(local) != 0:
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)  # 1:1 on a full node; ranks share a GPU only in a rehearsal
+    torch.cuda.set_device(gpu)
+    if pcs.lib().pcs_set_device(gpu) != 0:
         raise pcs.PcsError("pcs_set_device", -2, pcs.lib().pcs_last_error().decode())
-    dev = f"cuda:{local}"
+    dev = f"cuda:{gpu}"
     algo = pcs.XXH3_64 if args.algo == "xxh3" else pcs.XXH64
 
     w = Workload(args.config, algo, rank, args.pages_per_gpu, dev)

@@ -68,19 +68,25 @@ __device__ __forceinline__ uint64_t lo64(u32x4 v) { return ((uint64_t)v.y << 32)
 __device__ __forceinline__ uint64_t hi64(u32x4 v) { return ((uint64_t)v.w << 32) | v.z; }
 
 // Per-page output for every kernel: digest array, verdict array + first bad
-// index, or the digest stamped little-endian into page bytes [0, 8).
+// index, or the digest stamped little-endian into page bytes [0, 8).  Stores
+// are non-temporal: a plain 8-byte result store per page interleaved with the
+// page read stream cost ~5 % of read bandwidth, an nt store ~1-2 %
+// (profiles/r01/read_lab_stores.txt).
+template <typename T>
+__device__ __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
+
 __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_t stored, uint8_t* page_w,
                                      uint64_t* out, uint8_t* ok, unsigned long long* first_bad) {
     if (mode == kStamp) {
-        *reinterpret_cast<uint64_t*>(page_w) = h;
-        if (out) out[idx] = h;
+        st_nt(reinterpret_cast<uint64_t*>(page_w), h);
+        if (out) st_nt(out + idx, h);
     } else if (mode == kValidate) {
         const bool good = (h == stored);
-        ok[idx] = good ? 1 : 0;
-        if (out) out[idx] = h;
+        st_nt(ok + idx, (uint8_t)(good ? 1 : 0));
+        if (out) st_nt(out + idx, h);
         if (!good && first_bad) atomicMin(first_bad, (unsigned long long)idx);
     } else {
-        out[idx] = h;
+        st_nt(out + idx, h);
     }
 }
 
@@ -268,17 +274,45 @@ __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
     return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
 }
 
+// Block tile = 16 consecutive pages (one per group).  The loop runs over
+// tiles, so its trip count is uniform across the block and the barriers below
+// cannot diverge.  Digest / verdict mode stages the tile's 16 results in LDS
+// and writes them as one coalesced non-temporal store (128 B of digests or
+// 16 B of verdicts) instead of 16 scattered 8-byte stores.
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                    unsigned long long* first_bad) {
+    __shared__ uint64_t tile_h[16];
+    __shared__ uint8_t tile_ok[16];
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
-    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
-        const uint8_t* page = pages + pg * (uint64_t)P;
-        uint64_t stored = 0;
-        const uint64_t h = xxh3_page_fixed<P, NT>(page, L, stored);
-        if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+    const int grp = threadIdx.x >> 4;
+    const uint64_t ntiles = (n + 15) / 16;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t pg = t * 16 + grp;
+        if (pg < n) {
+            const uint8_t* page = pages + pg * (uint64_t)P;
+            uint64_t stored = 0;
+            const uint64_t h = xxh3_page_fixed<P, NT>(page, L, stored);
+            if (L.g == 0) {
+                if (MODE == kStamp) {
+                    emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+                } else {
+                    tile_h[grp] = h;
+                    tile_ok[grp] = (h == stored) ? 1 : 0;
+                    if (MODE == kValidate && h != stored && first_bad) atomicMin(first_bad, (unsigned long long)pg);
+                }
+            }
+        }
+        if (MODE != kStamp) {
+            __syncthreads();
+            const uint64_t i = t * 16 + threadIdx.x;
+            if (threadIdx.x < 16 && i < n) {
+                if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
+                if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -800,7 +834,7 @@ bool use_nt64() { return g_tune[4].load(std::memory_order_relaxed) != 0; }
 template <int MODE, bool NT>
 hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
                              unsigned long long* fb, hipStream_t s) {
-    const unsigned grid = page_grid(n, kBlock / 16, 1, P);
+    const unsigned grid = page_grid(n, kBlock / 16, 1, P);  // kBlock/16 = one 16-page tile per block
     switch (P) {
 #define CASE(SZ)                                                                                             \
     case SZ:                                                                                                 \

@@ -52,6 +52,61 @@ __global__ __launch_bounds__(256) void k_group16(const uint8_t* __restrict__ pag
     }
 }
 
+// A2: as A, but every page writes its 8-byte result (lane 0 of the group),
+// or (STAGED) the block's 16 results are staged in LDS and written by 16 lanes
+// of wave 0 as one 128-byte store.
+template <int P, bool STAGED>
+__global__ __launch_bounds__(256) void k_group16_store(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    __shared__ uint64_t res[16];
+    const int g = threadIdx.x & 15;
+    const uint64_t pg = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    uint32_t r = 0;
+    if (pg < n) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * P) + g;
+        u32x4 d[P / 256];
+#pragma unroll
+        for (int c = 0; c < P / 256; ++c) d[c] = ld<true>(base + c * 16);
+#pragma unroll
+        for (int c = 0; c < P / 256; ++c) r += fold(d[c]);
+    }
+    if constexpr (STAGED) {
+        if (g == 0) res[threadIdx.x >> 4] = r;
+        __syncthreads();
+        const uint64_t first = (uint64_t)blockIdx.x * 16;
+        if (threadIdx.x < 16 && first + threadIdx.x < n) out[first + threadIdx.x] = res[threadIdx.x];
+    } else {
+        if (g == 0 && pg < n) out[pg] = r;
+    }
+}
+
+// A3: each block hashes 16*M contiguous pages (M rounds of 16), keeps the
+// results in LDS and writes them as one 128*M-byte burst at the end.
+template <int P, int M, bool NTST>
+__global__ __launch_bounds__(256) void k_group16_batchstore(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    __shared__ uint64_t res[16 * M];
+    const int g = threadIdx.x & 15;
+    const uint64_t first = (uint64_t)blockIdx.x * 16 * M;
+    for (int m = 0; m < M; ++m) {
+        const uint64_t pg = first + m * 16 + (threadIdx.x >> 4);
+        uint32_t r = 0;
+        if (pg < n) {
+            const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * P) + g;
+            u32x4 d[P / 256];
+#pragma unroll
+            for (int c = 0; c < P / 256; ++c) d[c] = ld<true>(base + c * 16);
+#pragma unroll
+            for (int c = 0; c < P / 256; ++c) r += fold(d[c]);
+        }
+        if (g == 0) res[m * 16 + (threadIdx.x >> 4)] = r;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 16 * M; i += 256)
+        if (first + i < n) {
+            if constexpr (NTST) __builtin_nontemporal_store(res[i], out + first + i);
+            else out[first + i] = res[i];
+        }
+}
+
 // B: one page per wave, 1 KiB contiguous per wave-instruction
 template <int P, bool NT>
 __global__ __launch_bounds__(256) void k_wavepage(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
@@ -225,6 +280,13 @@ int main(int argc, char** argv) {
         add("quad64 nt U16 nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_quad64<4096, true, 16>), dim3(grid), dim3(256), 0, st, pages, n, out); });
         add("quad64 nt U4 nonpersistent", [=](hipStream_t st) { hipLaunchKernelGGL((k_quad64<4096, true, 4>), dim3(grid), dim3(256), 0, st, pages, n, out); });
     }
+    add("group16 nt store-per-page", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_store<4096, false>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
+    add("group16 nt store-staged128", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_store<4096, true>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
+    add("batchstore M=4", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 4, false>), dim3(n / 64), dim3(256), 0, st, pages, n, out); });
+    add("batchstore M=16", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 16, false>), dim3(n / 256), dim3(256), 0, st, pages, n, out); });
+    add("batchstore M=64", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 64, false>), dim3(n / 1024), dim3(256), 0, st, pages, n, out); });
+    add("batchstore M=16 nt-store", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 16, true>), dim3(n / 256), dim3(256), 0, st, pages, n, out); });
+    add("batchstore M=1 nt-store", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 1, true>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
     add("PRODUCT pcs_read_ceiling_dev", [=](hipStream_t st) { pcs_read_ceiling_dev(pages, 4096, n, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh3", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 0, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh64", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 1, out, (pcs_stream_t)st); });
