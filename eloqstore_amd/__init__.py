@@ -57,6 +57,15 @@ _SIGS = {
     "pcs_gen_desc_dev": [_vp, _vp, _vp, _u64, _u64, _u64, _vp],
     "pcs_flip_byte_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
     "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
+    "pcs_batch_create": [_P(_vp)],
+    "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32],
+    "pcs_batch_poll": [_vp],
+    "pcs_batch_wait": [_vp],
+    "pcs_batch_result": [_vp, _vp, _vp, _vp],
+    "pcs_batch_destroy": [_vp],
+    "pcs_manifest_checksum_dev": [_vp, _u64, _vp, _vp],
+    "pcs_manifest_checksum_host": [_vp, _u64, _P(_u64)],
+    "pcs_manifest_validate_host": [_vp, _u64, _P(_i32)],
     "pcs_set_tuning": [_i32, ctypes.c_int64],
     "pcs_get_tuning": [_i32],
     "pcs_version": [],
@@ -225,6 +234,70 @@ def flip_byte(pages, page_size: int, n: int, every: int, byte_offset: int = 10, 
 
 def read_ceiling(pages, page_size: int, n: int, out, stream=None) -> None:
     _call("pcs_read_ceiling_dev", _ptr(pages), page_size, n, _ptr(out), _stream(stream))
+
+
+def manifest_checksum_host(content: bytes) -> int:
+    """ManifestBuilder::CalcChecksum (root_meta.cpp:150-174) on the GPU."""
+    buf = (ctypes.c_char * max(1, len(content))).from_buffer_copy(content or b"\0")
+    out = ctypes.c_uint64(0)
+    _call("pcs_manifest_checksum_host", buf, len(content), ctypes.byref(out))
+    return out.value
+
+
+def manifest_validate_host(record: bytes) -> bool:
+    buf = (ctypes.c_char * max(1, len(record))).from_buffer_copy(record or b"\0")
+    v = ctypes.c_int(0)
+    _call("pcs_manifest_validate_host", buf, len(record), ctypes.byref(v))
+    return bool(v.value)
+
+
+class Batch:
+    """Asynchronous host batch (pcs_batch_*): submit, poll without blocking, read results."""
+
+    DIGEST, VALIDATE, STAMP = 0, 1, 2
+
+    def __init__(self):
+        self._b = ctypes.c_void_p()
+        _call("pcs_batch_create", ctypes.byref(self._b))
+        self._keep = None
+        self.n = 0
+
+    def submit(self, mode: int, pages: list, page_size: int, algo: int = XXH3_64) -> None:
+        arr, keep = _page_ptrs(pages)
+        self._keep = (arr, keep)
+        self.n = len(pages)
+        self.mode = mode
+        _call("pcs_batch_submit", self._b, mode, arr, page_size, len(pages), algo)
+
+    def poll(self) -> bool:
+        rc = lib().pcs_batch_poll(self._b)
+        if rc < 0:
+            _check("pcs_batch_poll", rc)
+        return rc == 1
+
+    def wait(self) -> None:
+        _call("pcs_batch_wait", self._b)
+
+    def result(self):
+        fb = ctypes.c_uint64(0)
+        if self.mode == self.VALIDATE:
+            ok = (ctypes.c_uint8 * max(1, self.n))()
+            _call("pcs_batch_result", self._b, ok, None, ctypes.byref(fb))
+            return list(ok)[: self.n], (None if fb.value == (1 << 64) - 1 else fb.value)
+        dig = (ctypes.c_uint64 * max(1, self.n))()
+        _call("pcs_batch_result", self._b, None, dig, ctypes.byref(fb))
+        return list(dig)[: self.n]
+
+    def close(self) -> None:
+        if self._b:
+            lib().pcs_batch_destroy(self._b)
+            self._b = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ---- host-memory forms (reference call surface) ------------------------------

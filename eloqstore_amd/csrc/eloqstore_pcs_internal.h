@@ -26,6 +26,8 @@ hipError_t run_gen_desc(uint8_t* base, const uint64_t* off, const uint32_t* len,
                         uint64_t first_page, hipStream_t s);
 hipError_t run_flip(uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t every, uint64_t byte_off,
                     hipStream_t s);
+// ManifestBuilder::CalcChecksum over a device-resident content buffer
+hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hipStream_t s);
 int set_tuning(int key, int64_t value);
 int64_t get_tuning(int key);
 hipError_t run_read_ceiling(const uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t* out, hipStream_t s);

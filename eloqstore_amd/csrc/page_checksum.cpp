@@ -59,4 +59,62 @@ void PageDigests(std::span<const char* const> pages, size_t page_size, uint64_t*
         die("PageDigests", rc);
 }
 
+ChecksumBatch::ChecksumBatch() {
+    if (int rc = pcs_batch_create(&batch_)) die("ChecksumBatch", rc);
+}
+
+ChecksumBatch::~ChecksumBatch() { pcs_batch_destroy(batch_); }
+
+void ChecksumBatch::SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash) {
+    n_ = pages.size();
+    validate_ = true;
+    collected_ = false;
+    ok_.assign(n_, 0);
+    if (int rc = pcs_batch_submit(batch_, PCS_BATCH_VALIDATE, reinterpret_cast<const void* const*>(pages.data()),
+                                  page_size, n_, static_cast<int>(hash)))
+        die("ChecksumBatch::SubmitValidate", rc);
+}
+
+void ChecksumBatch::SubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash) {
+    n_ = pages.size();
+    validate_ = false;
+    collected_ = false;
+    if (int rc = pcs_batch_submit(batch_, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(pages.data()),
+                                  page_size, n_, static_cast<int>(hash)))
+        die("ChecksumBatch::SubmitStamp", rc);
+}
+
+void ChecksumBatch::Collect() {
+    if (collected_) return;
+    uint64_t fb = UINT64_MAX;
+    if (int rc = pcs_batch_result(batch_, validate_ ? ok_.data() : nullptr, nullptr, &fb))
+        die("ChecksumBatch::Collect", rc);
+    first_bad_ = fb == UINT64_MAX ? n_ : static_cast<size_t>(fb);
+    collected_ = true;
+}
+
+bool ChecksumBatch::Poll() {
+    const int rc = pcs_batch_poll(batch_);
+    if (rc < 0) die("ChecksumBatch::Poll", rc);
+    if (rc == 1) Collect();
+    return rc == 1;
+}
+
+void ChecksumBatch::Wait() {
+    if (int rc = pcs_batch_wait(batch_)) die("ChecksumBatch::Wait", rc);
+    Collect();
+}
+
+uint64_t ManifestChecksum(std::string_view content) {
+    uint64_t h = 0;
+    if (int rc = pcs_manifest_checksum_host(content.data(), content.size(), &h)) die("ManifestChecksum", rc);
+    return h;
+}
+
+bool ValidateManifestRecord(std::string_view record) {
+    int valid = 0;
+    if (int rc = pcs_manifest_validate_host(record.data(), record.size(), &valid)) die("ValidateManifestRecord", rc);
+    return valid != 0;
+}
+
 }  // namespace eloqstore

@@ -279,6 +279,64 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
     return rc;
 }
 
+// Device copy of one host buffer + a result word, for the manifest host API.
+int manifest_host(const void* content, uint64_t len, uint64_t* out) {
+    if (int rc = require_device()) return rc;
+    if (!out || (len && !content)) return fail(PCS_ERR_INVALID, "null pointer");
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    uint8_t* d = nullptr;
+    uint64_t* d_out = nullptr;
+    e = hipMallocAsync(reinterpret_cast<void**>(&d_out), 8, s);
+    if (e == hipSuccess && len) e = hipMallocAsync(reinterpret_cast<void**>(&d), len, s);
+    if (e == hipSuccess && len) e = hipMemcpyAsync(d, content, len, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = pcs::run_manifest(d, len, d_out, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (d) (void)hipFreeAsync(d, s);
+    if (d_out) (void)hipFreeAsync(d_out, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return finish(e, "manifest checksum");
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// asynchronous batches
+// ---------------------------------------------------------------------------
+struct pcs_batch {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t* h_pages = nullptr;
+    uint8_t* d_pages = nullptr;
+    uint64_t* h_dig = nullptr;
+    uint64_t* d_dig = nullptr;
+    uint8_t* h_ok = nullptr;
+    uint8_t* d_ok = nullptr;
+    size_t cap_bytes = 0, cap_n = 0;
+    std::vector<void*> stamp_pages;
+    uint64_t n = 0, P = 0, first_bad = UINT64_MAX;
+    int mode = 0, state = 0;  // 0 idle, 1 in flight, 2 done, -1 failed
+};
+
+namespace {
+int batch_finalize(pcs_batch* b) {
+    b->first_bad = UINT64_MAX;
+    if (b->mode == PCS_BATCH_VALIDATE) {
+        for (uint64_t i = 0; i < b->n; ++i)
+            if (!b->h_ok[i]) {
+                b->first_bad = i;
+                break;
+            }
+    } else if (b->mode == PCS_BATCH_STAMP) {
+        for (uint64_t i = 0; i < b->n; ++i) std::memcpy(b->stamp_pages[i], &b->h_dig[i], 8);  // EncodeFixed64
+    }
+    b->state = 2;
+    return 1;
+}
 }  // namespace
 
 extern "C" {
@@ -358,6 +416,179 @@ int pcs_pages_digest_host(const void* const* pages, uint64_t page_size, uint64_t
                           uint64_t* digests) {
     if (n_pages && !digests) return fail(PCS_ERR_INVALID, "digests is null");
     return host_batch(0, pages, page_size, n_pages, algo, nullptr, nullptr, digests);
+}
+
+int pcs_batch_create(pcs_batch** out) {
+    if (!out) return fail(PCS_ERR_INVALID, "out is null");
+    *out = nullptr;
+    if (int rc = require_device()) return rc;
+    auto* b = new pcs_batch();
+    hipError_t e = hipGetDevice(&b->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        pcs_batch_destroy(b);
+        return hip_fail(e, "pcs_batch_create");
+    }
+    *out = b;
+    return PCS_OK;
+}
+
+int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo) {
+    if (!b) return fail(PCS_ERR_INVALID, "batch is null");
+    if (b->state == 1) return fail(PCS_ERR_INVALID, "batch already in flight");
+    if (mode < 0 || mode > 2) return fail(PCS_ERR_INVALID, "bad batch mode");
+    if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
+    if (P < 8 || P > 0xFFFFFFFFull) return fail(PCS_ERR_INVALID, "page_size must be in [8, 2^32)");
+    if (n && !pages) return fail(PCS_ERR_INVALID, "pages is null");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!pages[i]) return fail(PCS_ERR_INVALID, "null page pointer in batch");
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
+    hipError_t e = hipSuccess;
+    if (n * P > b->cap_bytes) {
+        (void)hipHostFree(b->h_pages);
+        (void)hipFree(b->d_pages);
+        b->h_pages = nullptr;
+        b->d_pages = nullptr;
+        b->cap_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_pages), n * P, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&b->d_pages), n * P) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "batch staging allocation failed");
+        b->cap_bytes = n * P;
+    }
+    if (n > b->cap_n) {
+        (void)hipHostFree(b->h_dig);
+        (void)hipFree(b->d_dig);
+        (void)hipHostFree(b->h_ok);
+        (void)hipFree(b->d_ok);
+        b->h_dig = nullptr; b->d_dig = nullptr; b->h_ok = nullptr; b->d_ok = nullptr;
+        b->cap_n = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&b->d_dig), n * 8) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&b->h_ok), n, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&b->d_ok), n) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "batch result allocation failed");
+        b->cap_n = n;
+    }
+    b->mode = mode;
+    b->n = n;
+    b->P = P;
+    b->stamp_pages.assign(n, nullptr);
+    if (mode == PCS_BATCH_STAMP)
+        for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
+    if (n == 0) {
+        b->state = 2;
+        b->first_bad = UINT64_MAX;
+        return PCS_OK;
+    }
+    for (uint64_t i = 0; i < n; ++i) std::memcpy(b->h_pages + i * P, pages[i], P);
+    hipStream_t s = b->stream;
+    e = hipMemcpyAsync(b->d_pages, b->h_pages, n * P, hipMemcpyHostToDevice, s);
+    const int kmode = mode == PCS_BATCH_VALIDATE ? 1 : 0;
+    if (e == hipSuccess) e = pcs::run_pages(kmode, algo, b->d_pages, P, n, b->d_dig, b->d_ok, nullptr, s);
+    if (e == hipErrorNotSupported) {
+        (void)hipGetLastError();
+        if (int rc = pages_common(kmode, b->d_pages, P, n, algo, b->d_dig, b->d_ok, nullptr,
+                                  reinterpret_cast<pcs_stream_t>(s))) {
+            b->state = -1;
+            return rc;
+        }
+        e = hipSuccess;
+    }
+    if (e == hipSuccess)
+        e = kmode ? hipMemcpyAsync(b->h_ok, b->d_ok, n, hipMemcpyDeviceToHost, s)
+                  : hipMemcpyAsync(b->h_dig, b->d_dig, n * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(b->done, s);
+    if (e != hipSuccess) {
+        b->state = -1;
+        return hip_fail(e, "pcs_batch_submit");
+    }
+    b->state = 1;
+    return PCS_OK;
+}
+
+int pcs_batch_poll(pcs_batch* b) {
+    if (!b) return fail(PCS_ERR_INVALID, "batch is null");
+    if (b->state == 2) return 1;
+    if (b->state != 1) return fail(PCS_ERR_INVALID, "no batch submitted");
+    const hipError_t e = hipEventQuery(b->done);
+    if (e == hipErrorNotReady) return 0;
+    if (e != hipSuccess) {
+        b->state = -1;
+        return hip_fail(e, "pcs_batch_poll");
+    }
+    return batch_finalize(b);
+}
+
+int pcs_batch_wait(pcs_batch* b) {
+    if (!b) return fail(PCS_ERR_INVALID, "batch is null");
+    if (b->state == 2) return PCS_OK;
+    if (b->state != 1) return fail(PCS_ERR_INVALID, "no batch submitted");
+    const hipError_t e = hipEventSynchronize(b->done);
+    if (e != hipSuccess) {
+        b->state = -1;
+        return hip_fail(e, "pcs_batch_wait");
+    }
+    batch_finalize(b);
+    return PCS_OK;
+}
+
+int pcs_batch_result(pcs_batch* b, uint8_t* ok, uint64_t* digests, uint64_t* first_bad) {
+    if (!b) return fail(PCS_ERR_INVALID, "batch is null");
+    if (b->state != 2) return fail(PCS_ERR_INVALID, "batch not complete");
+    if (ok) {
+        if (b->mode != PCS_BATCH_VALIDATE) return fail(PCS_ERR_INVALID, "verdicts exist only in validate mode");
+        std::memcpy(ok, b->h_ok, b->n);
+    }
+    if (digests) {
+        if (b->mode == PCS_BATCH_VALIDATE) return fail(PCS_ERR_INVALID, "digests exist in digest/stamp mode");
+        std::memcpy(digests, b->h_dig, b->n * 8);
+    }
+    if (first_bad) *first_bad = b->first_bad;
+    return PCS_OK;
+}
+
+int pcs_batch_destroy(pcs_batch* b) {
+    if (!b) return PCS_OK;
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    (void)hipHostFree(b->h_pages);
+    (void)hipFree(b->d_pages);
+    (void)hipHostFree(b->h_dig);
+    (void)hipFree(b->d_dig);
+    (void)hipHostFree(b->h_ok);
+    (void)hipFree(b->d_ok);
+    if (b->done) (void)hipEventDestroy(b->done);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+    return PCS_OK;
+}
+
+int pcs_manifest_checksum_dev(const void* d_content, uint64_t len, uint64_t* d_out, pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (!d_out || (len && !d_content)) return fail(PCS_ERR_INVALID, "null pointer");
+    return finish(pcs::run_manifest(static_cast<const uint8_t*>(d_content), len, d_out,
+                                    reinterpret_cast<hipStream_t>(stream)),
+                  "manifest checksum");
+}
+
+int pcs_manifest_checksum_host(const void* content, uint64_t len, uint64_t* out) {
+    return manifest_host(content, len, out);
+}
+
+int pcs_manifest_validate_host(const void* record, uint64_t size, int* valid) {
+    if (!valid || (size && !record)) return fail(PCS_ERR_INVALID, "null pointer");
+    constexpr uint64_t kHeaderBytes = 8 + 4 + 4 + 4;  // root_meta.h:61-63
+    if (size < kHeaderBytes) {
+        *valid = 0;
+        return PCS_OK;
+    }
+    uint64_t h = 0;
+    if (int rc = manifest_host(static_cast<const uint8_t*>(record) + 8, size - 8, &h)) return rc;
+    uint64_t stored;
+    std::memcpy(&stored, record, 8);  // DecodeFixed64
+    *valid = stored == h ? 1 : 0;
+    return PCS_OK;
 }
 
 int pcs_shard_range(uint64_t n, int world, int rank, uint64_t* begin, uint64_t* end) {

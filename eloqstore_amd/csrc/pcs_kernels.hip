@@ -561,6 +561,15 @@ __global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ 
     }
 }
 
+// long raw-range shape (k_xxh3_long, below); the lane kernel skips these
+constexpr int kLongWin = 64;             // blocks per window (64 KiB of input)
+constexpr uint32_t kLongMin = 2048;      // shorter ranges stay on the lane kernel
+constexpr int kQuadSwap1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);  // quad_perm [1,0,3,2]
+
+__device__ __forceinline__ bool xxh3_long_ok(const uint8_t* p, uint32_t L) {
+    return L >= kLongMin && ((uintptr_t)p % 8u) == 0;
+}
+
 // ---------------------------------------------------------------------------
 // generic single-lane XXH3_64bits / XXH64 over any byte range (any alignment)
 // ---------------------------------------------------------------------------
@@ -680,7 +689,8 @@ __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict_
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t o = off[i];
         const uint32_t L = len[i];
-        if (filter && (algo == 0 ? xxh3_fast_ok(o, L) : xxh64_fast_ok(o, L))) continue;
+        if (filter == 1 && (algo == 0 ? xxh3_fast_ok(o, L) : xxh64_fast_ok(o, L))) continue;
+        if (filter == 2 && xxh3_long_ok(base + o, L)) continue;
         const uint8_t* p = base + o;
         if ((uint32_t)skip > L) {  // page shorter than its digest header: never valid
             if (MODE == kValidate) {
@@ -700,6 +710,111 @@ __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict_
         } else {
             emit(MODE, i, h, stored, nullptr, out, ok, first_bad);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// XXH3 over long raw ranges: one workgroup per range
+// ---------------------------------------------------------------------------
+// For a single long input (a manifest chunk of up to 1 MiB,
+// root_meta.cpp:150-174; a whole object) the page kernels' one-group-per-input
+// mapping leaves the GPU idle.  XXH3's long loop (xxhash.h:5988-6017) is a
+// chain acc <- scramble(acc + S_b) over 1 KiB blocks whose block sums S_b are
+// independent, so the 16 groups of a workgroup compute S_b for a window of
+// 64 blocks in parallel into LDS and 8 lanes then run the short serial
+// scramble chain over the window.
+//
+// Lane g of a group loads words g + 16j (j < 8) of a block: 128 contiguous
+// bytes per group-instruction.  Word w = g + 16j has stripe s = g/8 + 2j and
+// accumulator lane l = g & 7, so a lane's multiply terms all go to acc[l] and
+// its raw words to acc[l ^ 1]: one quad_perm swap and one row_ror:8 fold give
+// each lane l < 8 the block sum of acc[l].
+
+// block sum for the lane's accumulator l = g & 7 (valid in lanes 0..7)
+__device__ __forceinline__ uint64_t xxh3_long_block(const uint64_t* __restrict__ blk, int g, int nstripes) {
+    const int l = g & 7;
+    uint64_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = (g / 8 + 2 * j < nstripes) ? blk[g + 16 * j] : 0;
+    uint64_t M = 0, R = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int s = g / 8 + 2 * j;
+        if (s < nstripes) {
+            M += mul32x32(w[j] ^ c_keys.acc[s + l]);
+            R += w[j];
+        }
+    }
+    uint64_t T = M + dpp64<kQuadSwap1>(R);
+    T += dpp64<kRowRor8>(T);
+    return T;
+}
+
+__global__ __launch_bounds__(256) void k_xxh3_long(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ len, uint64_t n,
+                                                  uint64_t* __restrict__ out) {
+    __shared__ uint64_t S[kLongWin][8];
+    const int tid = threadIdx.x, g = tid & 15, grp = tid >> 4;
+    for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const uint8_t* in8 = base + off[r];
+        const uint32_t L = len[r];
+        if (!xxh3_long_ok(in8, L)) continue;  // uniform over the workgroup
+        const uint64_t* in = reinterpret_cast<const uint64_t*>(in8);
+        const uint32_t nb = (L - 1) / 1024;
+        uint64_t acc = tid < 8 ? c_init_acc[tid] : 0;  // threads 0..7 own acc[tid]
+        for (uint32_t w0 = 0; w0 < nb; w0 += kLongWin) {
+            const int nw = (int)min((uint32_t)kLongWin, nb - w0);
+#pragma unroll
+            for (int i = 0; i < kLongWin / 16; ++i) {
+                const int b = grp + 16 * i;
+                if (b < nw) {
+                    const uint64_t T = xxh3_long_block(in + (size_t)(w0 + b) * 128, g, 16);
+                    if (g < 8) S[b][g] = T;
+                }
+            }
+            __syncthreads();
+            if (tid < 8)
+                for (int b = 0; b < nw; ++b) acc = xxh3_scramble(acc + S[b][tid], c_keys.scr[tid]);
+            __syncthreads();
+        }
+        if (grp == 0) {
+            const int nst = (int)(((L - 1) - 1024 * nb) / 64);
+            uint64_t T = xxh3_long_block(in + (size_t)nb * 128, g, nst);
+            // last stripe at input + L - 64, keyed with secret + 121 (xxhash.h:6013-6015)
+            uint64_t M = 0, R = 0;
+            if (g < 8) {
+                const uint64_t v = ld64(in8 + L - 64 + 8 * g);
+                M = mul32x32(v ^ c_keys.last[g]);
+                R = v;
+            }
+            T += M + dpp64<kQuadSwap1>(R);
+            acc += T;
+            // mergeAccs (xxhash.h:6029-6052): even lanes fold pairs (l, l + 1)
+            const uint64_t nxt = dpp64<kRowRor15>(acc);
+            uint64_t m = (g < 8 && (g & 1) == 0) ? mul_fold64(acc ^ c_keys.merge[g], nxt ^ c_keys.merge[g + 1]) : 0;
+            m += dpp64<kRowRor2>(m);
+            m += dpp64<kRowRor4>(m);  // lane 0..7: m0+m2+m4+m6 (lanes 0,2,4,6 of 0..7)
+            if (g == 6) out[r] = xxh3_avalanche((uint64_t)L * kP64_1 + m);
+        }
+        __syncthreads();
+    }
+}
+
+// Manifest record aggregate (ManifestBuilder::CalcChecksum, root_meta.cpp:150-174):
+// chunk digests folded serially, agg = rotl(agg, 1) ^ h; agg *= 0x9e3779b97f4a7c15.
+__global__ void k_manifest_fold(const uint64_t* __restrict__ chunk_h, uint64_t nchunks, uint64_t* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint64_t agg = 0;
+    for (uint64_t i = 0; i < nchunks; ++i) agg = (rotl64(agg, 1) ^ chunk_h[i]) * 0x9e3779b97f4a7c15ull;
+    *out = agg;
+}
+
+__global__ void k_make_chunks(uint64_t total, uint64_t chunk, uint64_t n, uint64_t* __restrict__ off,
+                              uint32_t* __restrict__ len) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        off[i] = i * chunk;
+        len[i] = (uint32_t)min(chunk, total - i * chunk);
     }
 }
 
@@ -915,10 +1030,44 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
                            1, out, ok, fb);
         return hipGetLastError();
     }
+    int filter = 0;
+    if (MODE == kDigest && algo == 0 && skip == 0) {
+        // raw XXH3 ranges: long ones get a workgroup each
+        const unsigned lgrid = grid_for(n, 1, 8);
+        hipLaunchKernelGGL(k_xxh3_long, dim3(lgrid), dim3(kBlock), 0, s, base, off, len, n, out);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        filter = 2;
+    }
     const unsigned grid = grid_for(n, kBlock, kBlocksPerCu);
-    hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip, 0,
-                       out, ok, fb);
+    hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip,
+                       filter, out, ok, fb);
     return hipGetLastError();
+}
+
+hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hipStream_t s) {
+    constexpr uint64_t kChunk = 1u << 20;  // kCheckSumBatchSize, root_meta.cpp:157
+    if (len == 0) return hipMemsetAsync(out, 0, 8, s);
+    const uint64_t n = (len + kChunk - 1) / kChunk;
+    uint64_t* off = nullptr;
+    uint32_t* ln = nullptr;
+    uint64_t* h = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&off), n * 8, s);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&ln), n * 4, s);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&h), n * 8, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, len, kChunk, n, off, ln);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = desc_impl<kDigest>(0, content, off, ln, n, 0, 0, h, nullptr, nullptr, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_manifest_fold, dim3(1), dim3(64), 0, s, h, n, out);
+        e = hipGetLastError();
+    }
+    if (off) (void)hipFreeAsync(off, s);
+    if (ln) (void)hipFreeAsync(ln, s);
+    if (h) (void)hipFreeAsync(h, s);
+    return e;
 }
 
 hipError_t run_desc(int mode, int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,

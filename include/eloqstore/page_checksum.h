@@ -22,6 +22,9 @@
 #include <cstdint>
 #include <span>
 #include <string_view>
+#include <vector>
+
+struct pcs_batch;  // include/eloqstore_pcs.h (global namespace, C ABI)
 
 namespace eloqstore {
 
@@ -48,5 +51,36 @@ void SetChecksums(std::span<char* const> pages, size_t page_size, PageHash hash 
 // Digests without touching the pages.
 void PageDigests(std::span<const char* const> pages, size_t page_size, uint64_t* digests_out,
                  PageHash hash = PageHash::XXH3_64);
+
+// Asynchronous batch for coroutine call sites: Submit, then Poll() from the
+// shard work loop (shard.cpp:67-130) until it returns true.  Pages must stay
+// valid until then; SubmitStamp writes the digests into them on completion.
+class ChecksumBatch {
+public:
+    ChecksumBatch();
+    ~ChecksumBatch();
+    ChecksumBatch(const ChecksumBatch&) = delete;
+    ChecksumBatch& operator=(const ChecksumBatch&) = delete;
+
+    void SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
+    void SubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
+    bool Poll();  // true once complete; never blocks
+    void Wait();
+    // Validate mode, after completion: index of the first corrupted page, or
+    // the batch size if every page matched.
+    size_t FirstBad() const { return first_bad_; }
+    const uint8_t* Verdicts() const { return ok_.data(); }
+
+private:
+    void Collect();
+    ::pcs_batch* batch_ = nullptr;
+    std::vector<uint8_t> ok_;
+    size_t n_ = 0, first_bad_ = 0;
+    bool validate_ = false, collected_ = false;
+};
+
+// ManifestBuilder::CalcChecksum / ValidateChecksum (src/storage/root_meta.cpp:138-174).
+uint64_t ManifestChecksum(std::string_view content);
+bool ValidateManifestRecord(std::string_view record);
 
 }  // namespace eloqstore

@@ -121,6 +121,40 @@ int pcs_pages_stamp_host(void *const *pages, uint64_t page_size, uint64_t n_page
 int pcs_pages_digest_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
                           int algo, uint64_t *digests);
 
+/* ---- asynchronous host batches (shard-loop integration) --------------------
+ * EloqStore's shard thread never blocks: its work loop is Submit() ->
+ * PollComplete() -> ExecuteReadyTasks() (src/storage/shard.cpp:67-130), and
+ * a ReadPages / FlushBatchPages coroutine yields while I/O is in flight.  A
+ * pcs_batch is the checksum analogue: submit gathers the pages (or DMAs a
+ * pinned contiguous run directly), enqueues H2D + kernel + D2H on the batch's
+ * own stream and returns; poll answers "done?" without blocking.  One batch
+ * object holds one batch in flight; create several for more concurrency.
+ * Pages must stay valid until the batch completes (stamp writes the digests
+ * into them when poll/wait observes completion). */
+typedef struct pcs_batch pcs_batch;
+enum pcs_batch_mode { PCS_BATCH_DIGEST = 0, PCS_BATCH_VALIDATE = 1, PCS_BATCH_STAMP = 2 };
+int pcs_batch_create(pcs_batch **out);  /* on the calling thread's current device */
+int pcs_batch_submit(pcs_batch *b, int mode, const void *const *pages, uint64_t page_size,
+                     uint64_t n_pages, int algo);
+int pcs_batch_poll(pcs_batch *b);   /* 1 = done, 0 = in flight, < 0 = error */
+int pcs_batch_wait(pcs_batch *b);   /* blocks until done; PCS_OK or error */
+/* After completion: verdicts / digests (either may be NULL) and the first
+ * failing index (UINT64_MAX if none, validate mode). */
+int pcs_batch_result(pcs_batch *b, uint8_t *ok, uint64_t *digests, uint64_t *first_bad);
+int pcs_batch_destroy(pcs_batch *b);
+
+/* ---- manifest record checksum (next row: SURVEY.md §8f-3) -----------------
+ * ManifestBuilder::CalcChecksum (src/storage/root_meta.cpp:150-174): XXH3-64
+ * of each <= 1 MiB chunk of the content, folded as agg = rotl(agg, 1) ^ h;
+ * agg *= 0x9e3779b97f4a7c15; empty content -> 0.  Chunks >= 2 KiB at 8-byte
+ * alignment run on the long-range kernel (a workgroup per chunk). */
+int pcs_manifest_checksum_dev(const void *d_content, uint64_t len, uint64_t *d_out, pcs_stream_t stream);
+int pcs_manifest_checksum_host(const void *content, uint64_t len, uint64_t *out);
+/* ManifestBuilder::ValidateChecksum (root_meta.cpp:138-148): a record is
+ * checksum(8) | root(4) | ttl_root(4) | len(4) | payload; records shorter than
+ * the 20-byte header never validate. */
+int pcs_manifest_validate_host(const void *record, uint64_t size, int *valid);
+
 /* ---- sharding ------------------------------------------------------------
  * Contiguous page range [begin, end) of rank `rank` of `world` for n pages:
  * begin = floor(rank * n / world).  Pages are independent, so G GPUs hash G

@@ -33,7 +33,8 @@ def test_cpp_dropin_symbols_exported():
                          check=True).stdout
     for sym in ("eloqstore::SetChecksum(std::basic_string_view<char, std::char_traits<char> >)",
                 "eloqstore::ValidateChecksum(std::basic_string_view<char, std::char_traits<char> >)",
-                "eloqstore::ValidateChecksums(", "eloqstore::SetChecksums(", "eloqstore::PageDigests("):
+                "eloqstore::ValidateChecksums(", "eloqstore::SetChecksums(", "eloqstore::PageDigests(",
+                "eloqstore::ChecksumBatch::Poll()", "eloqstore::ManifestChecksum(", "eloqstore::ValidateManifestRecord("):
         assert sym in out, sym
 
 

@@ -370,3 +370,87 @@ def test_host_direct_pinned_path(algo):
     fb = ctypes.c_uint64(0)
     rc = pcs.lib().pcs_pages_validate_host(ptrs.ctypes.data, P, n, algo, ok.ctypes.data, ctypes.byref(fb))
     assert rc == 0 and fb.value == 777 and int((ok == 0).sum()) == 1
+
+
+def test_long_ranges_vs_oracle():
+    """Raw XXH3 ranges long enough for the workgroup-per-range kernel (>= 2 KiB,
+    8-byte aligned), every tail shape: full/partial last block, odd lengths
+    (unaligned last stripe), exact multiples of 1 KiB, 1 MiB manifest chunks."""
+    rng = np.random.default_rng(11)
+    lens = [2048, 2049, 2055, 2056, 3071, 3072, 3073, 4088, 4096, 5000, 65536, 65535 + 1024 * 3, 131072 + 17,
+            (1 << 20), (1 << 20) - 1, 1000000, 777777] + [int(x) for x in rng.integers(2048, 300000, size=40)]
+    offs, pos = [], 0
+    for i, L in enumerate(lens):
+        offs.append(pos + (8 if i % 3 == 1 else 0))  # mix 16-aligned and 8-mod-16 starts
+        pos = offs[-1] + L + 8
+        pos = (pos + 7) // 8 * 8
+    host = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
+    base = torch.from_numpy(host).to(DEV)
+    o = np.array(offs, dtype=np.uint64)
+    ln = np.array(lens, dtype=np.uint32)
+    got = u64(pcs.xxh3_64_ranges(base, torch.from_numpy(o.view(np.int64)).to(DEV),
+                                 torch.from_numpy(ln.view(np.int32)).to(DEV), len(lens)))
+    want = oracle.desc_raw_xxh3(host, o, ln)
+    assert np.array_equal(got, want), [lens[i] for i in np.nonzero(got != want)[0]]
+
+
+def test_manifest_api_vs_golden(golden):
+    mf = golden["manifest"]
+    longest = max(r[0] for r in mf["rows"])
+    buf = splitmix_words(mf["seed"], 0, longest // 8 + 8).view(np.uint8)
+    dbuf = torch.from_numpy(buf.copy()).to(DEV)
+    d_out = torch.empty(1, dtype=torch.int64, device=DEV)
+    for L, h in mf["rows"]:
+        assert pcs.manifest_checksum_host(buf[:L].tobytes()) == int(h, 16), L
+        pcs._call("pcs_manifest_checksum_dev", dbuf.data_ptr(), L, d_out.data_ptr(), pcs._stream(None))
+        assert int(u64(d_out)[0]) == int(h, 16), L
+
+
+def test_manifest_record_validate():
+    content = splitmix_words(5, 1, 40000).view(np.uint8).tobytes()[:300000]
+    for L in (0, 12, 4000, 300000 - 20):
+        rec = bytearray(8) + bytearray(content[: 12 + L])  # root|ttl|len + payload
+        h = pcs.manifest_checksum_host(bytes(rec[8:]))
+        assert h == oracle.manifest_checksum(bytes(rec[8:]))
+        rec[:8] = h.to_bytes(8, "little")
+        assert pcs.manifest_validate_host(bytes(rec))
+        rec[-1] ^= 0x80
+        assert not pcs.manifest_validate_host(bytes(rec))
+    assert not pcs.manifest_validate_host(b"\0" * 19)  # shorter than the 20-byte header
+
+
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+def test_async_batches(algo):
+    P = 4096
+    pages = [bytearray(splitmix_words(21, i, P // 8).tobytes()) for i in range(256)]
+    stamp = pcs.Batch()
+    stamp.submit(pcs.Batch.STAMP, pages, P, algo)
+    while not stamp.poll():
+        pass
+    for p in pages:
+        h = oracle.xxh3_64(bytes(p[8:])) if algo == 0 else oracle.xxh64(bytes(p[8:]))
+        assert int.from_bytes(p[:8], "little") == h
+    pages[99][2000] ^= 4
+    v1, v2 = pcs.Batch(), pcs.Batch()
+    v1.submit(pcs.Batch.VALIDATE, pages[:128], P, algo)
+    v2.submit(pcs.Batch.VALIDATE, pages[128:], P, algo)
+    v2.wait()
+    while not v1.poll():
+        pass
+    ok1, fb1 = v1.result()
+    ok2, fb2 = v2.result()
+    assert fb1 == 99 and sum(ok1) == 127 and fb2 is None and all(ok2)
+    d = pcs.Batch()
+    d.submit(pcs.Batch.DIGEST, pages[:10], P, algo)
+    d.wait()
+    want = [(oracle.xxh3_64 if algo == 0 else oracle.xxh64)(bytes(p[8:])) for p in pages[:10]]
+    assert d.result() == want
+    empty = pcs.Batch()
+    empty.submit(pcs.Batch.VALIDATE, [], P, algo)
+    assert empty.poll() and empty.result() == ([], None)
+
+
+def test_cpp_dropin_program():
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "dropin_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "dropin ok" in r.stdout, r.stdout + r.stderr
