@@ -136,6 +136,7 @@ TUNE_XXH3_BLOCKS_PER_CU = 1
 TUNE_XXH64_BLOCKS_PER_CU = 2
 TUNE_NT_LOADS = 3
 TUNE_XXH64_NT_LOADS = 4
+TUNE_STAMP_BYTES = 5
 
 
 def set_tuning(key: int, value: int) -> None:

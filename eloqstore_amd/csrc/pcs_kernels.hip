@@ -198,7 +198,7 @@ __device__ __forceinline__ uint64_t xxh3_merge(const Xxh3Lane& L, uint64_t Ae, u
 // following block and hands it on, so no byte is loaded twice.
 template <int P, bool NT>
 __device__ __forceinline__ uint64_t xxh3_page_fixed(const uint8_t* __restrict__ page, const Xxh3Lane& L,
-                                                    uint64_t& stored) {
+                                                    uint64_t& stored, u32x4& first) {
     constexpr int NB = (P - 9) / 1024;   // full blocks (xxhash.h:5996)
     constexpr int R = P / 256 - 4 * NB;  // chunks in the final block, 1..4
     constexpr int TB = NB + 1;
@@ -206,6 +206,7 @@ __device__ __forceinline__ uint64_t xxh3_page_fixed(const uint8_t* __restrict__ 
     uint64_t Ae = L.init_e, Ao = L.init_o;
     u32x4 head = ld16<NT>(base);  // chunk 0 of the next block to fold
     stored = lo64(head);
+    first = head;
 #pragma unroll
     for (int b0 = 0; b0 < TB; b0 += 4) {
         constexpr int kMaxBatch = 4;
@@ -279,29 +280,53 @@ __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
 // cannot diverge.  Digest / verdict mode stages the tile's 16 results in LDS
 // and writes them as one coalesced non-temporal store (128 B of digests or
 // 16 B of verdicts) instead of 16 scattered 8-byte stores.
+//
+// When the grid covers every tile once, tiles are renumbered so that the
+// blocks sharing an XCD (blockIdx % 8) stream one contiguous slice of the
+// batch (cdna_hip_programming.md T1, bijective form); measured +1 %.
+//
+// Stamp (SetChecksum) rewrites the first stamp_bytes of the page from the
+// registers that already hold them, with the digest in bytes [0, 8): a bare
+// 8-byte store per page is a partial-line write the memory side must merge
+// (measured -26 % vs digest mode); whole-line rewrites avoid the merge.
+__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t nb) {
+    const uint64_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   unsigned long long* first_bad) {
+                                                   unsigned long long* first_bad, int stamp_bytes) {
     __shared__ uint64_t tile_h[16];
     __shared__ uint8_t tile_ok[16];
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const int grp = threadIdx.x >> 4;
     const uint64_t ntiles = (n + 15) / 16;
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
         const uint64_t pg = t * 16 + grp;
         if (pg < n) {
             const uint8_t* page = pages + pg * (uint64_t)P;
             uint64_t stored = 0;
-            const uint64_t h = xxh3_page_fixed<P, NT>(page, L, stored);
-            if (L.g == 0) {
-                if (MODE == kStamp) {
-                    emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
-                } else {
-                    tile_h[grp] = h;
-                    tile_ok[grp] = (h == stored) ? 1 : 0;
-                    if (MODE == kValidate && h != stored && first_bad) atomicMin(first_bad, (unsigned long long)pg);
+            u32x4 first;
+            const uint64_t h = xxh3_page_fixed<P, NT>(page, L, stored, first);
+            if (MODE == kStamp) {
+                if (stamp_bytes <= 8) {
+                    if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+                } else if (L.g * 16 < stamp_bytes) {
+                    if (L.g == 0) {
+                        first.x = (uint32_t)h;
+                        first.y = (uint32_t)(h >> 32);
+                        if (out) st_nt(out + pg, h);
+                    }
+                    st_nt(reinterpret_cast<u32x4*>(const_cast<uint8_t*>(page)) + L.g, first);
                 }
+            } else if (L.g == 0) {
+                tile_h[grp] = h;
+                tile_ok[grp] = (h == stored) ? 1 : 0;
+                if (MODE == kValidate && h != stored && first_bad) atomicMin(first_bad, (unsigned long long)pg);
             }
         }
         if (MODE != kStamp) {
@@ -322,8 +347,11 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
                                                     uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                     unsigned long long* first_bad) {
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
-    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+    const uint64_t ntiles = (n + 15) / 16;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 16 + (threadIdx.x >> 4);
+        if (pg >= n) continue;
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
         const uint64_t h = xxh3_page_rt<NT>(page, P, L, stored);
@@ -339,8 +367,11 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                   unsigned long long* first_bad) {
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
-    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+    const uint64_t ntiles = (n + 15) / 16;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 16 + (threadIdx.x >> 4);
+        if (pg >= n) continue;
         const uint64_t o = off[pg];
         const uint32_t P = len[pg];
         if (!xxh3_fast_ok(o, P)) continue;
@@ -533,8 +564,11 @@ __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict_
                                                      uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                      unsigned long long* first_bad) {
     const int a = threadIdx.x & 3;
-    const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x >> 2);
-    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; pg < n; pg += nquads) {
+    const uint64_t ntiles = (n + 63) / 64;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 64 + (threadIdx.x >> 2);
+        if (pg >= n) continue;
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
         const uint64_t h = LINES ? xxh64_page_lines<NT>(page, P, a, stored) : xxh64_page<false>(page, P, a, stored);
@@ -548,8 +582,11 @@ __global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ 
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                    unsigned long long* first_bad) {
     const int a = threadIdx.x & 3;
-    const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x >> 2);
-    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; pg < n; pg += nquads) {
+    const uint64_t ntiles = (n + 63) / 64;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 64 + (threadIdx.x >> 2);
+        if (pg >= n) continue;
         const uint64_t o = off[pg];
         const uint32_t P = len[pg];
         if (!xxh64_fast_ok(o, P)) continue;
@@ -859,14 +896,24 @@ __global__ void k_flip_byte(uint8_t* pages, uint64_t P, uint64_t n, uint64_t eve
     if (p < n) pages[p * P + byte_off] ^= 0xFF;
 }
 
+// Second pass of a two-pass stamp: page i bytes [0, 8) = digest[i].
+__global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pages, uint64_t P, uint64_t n,
+                                                      const uint64_t* __restrict__ dig) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) st_nt(reinterpret_cast<uint64_t*>(pages + i * P), dig[i]);
+}
+
 // Same access pattern and output as k_xxh3_fixed<P, kDigest> minus the hash:
 // the achievable HBM read rate for this layout (roofline "measured ceiling").
 template <int P, bool NT>
 __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
                                                      uint64_t* __restrict__ out) {
     const int g = threadIdx.x & 15;
-    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x >> 4);
-    for (uint64_t pg = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+    const uint64_t ntiles = (n + 15) / 16;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 16 + (threadIdx.x >> 4);
+        if (pg >= n) continue;
         const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P) + g;
         uint32_t x = 0, y = 0, z = 0, w = 0;
 #pragma unroll
@@ -879,7 +926,7 @@ __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict_
         r ^= dpp64<kRowRor2>(r);
         r ^= dpp64<kRowRor4>(r);
         r ^= dpp64<kRowRor8>(r);
-        if (g == 0) out[pg] = r;
+        if (g == 0) st_nt(out + pg, r);
     }
 }
 
@@ -922,7 +969,8 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-std::atomic<int64_t> g_tune[8] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1, /*xxh64 nt*/ 0, 0, 0, 0};
+std::atomic<int64_t> g_tune[8] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1, /*xxh64 nt*/ 0,
+                                  /*stamp bytes (0 = two-pass)*/ 0, 0, 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= 8 || value < 0) return -1;
@@ -950,10 +998,11 @@ template <int MODE, bool NT>
 hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
                              unsigned long long* fb, hipStream_t s) {
     const unsigned grid = page_grid(n, kBlock / 16, 1, P);  // kBlock/16 = one 16-page tile per block
+    const int sb = (int)std::min<int64_t>(g_tune[5].load(std::memory_order_relaxed), 256);
     switch (P) {
 #define CASE(SZ)                                                                                             \
     case SZ:                                                                                                 \
-        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb); \
+        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb, sb); \
         break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
@@ -974,6 +1023,23 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
     const bool aligned16 = ((uintptr_t)pages % 16) == 0;
     const bool aligned8 = ((uintptr_t)pages % 8) == 0;
     if (algo == 0 && aligned16 && P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull) {
+        if (MODE == kStamp && g_tune[5].load(std::memory_order_relaxed) == 0) {
+            // two-pass stamp: digests into a compact array (the fast digest
+            // kernel), then one scattered 8-byte write per page
+            uint64_t* dig = out;
+            hipError_t e = hipSuccess;
+            if (!dig) e = hipMallocAsync(reinterpret_cast<void**>(&dig), n * 8, s);
+            if (e == hipSuccess)
+                e = use_nt() ? launch_xxh3_pages<kDigest, true>(P, pages, n, dig, nullptr, nullptr, s)
+                             : launch_xxh3_pages<kDigest, false>(P, pages, n, dig, nullptr, nullptr, s);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_scatter_stamp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                                   const_cast<uint8_t*>(pages), P, n, dig);
+                e = hipGetLastError();
+            }
+            if (dig && dig != out) (void)hipFreeAsync(dig, s);
+            return e;
+        }
         return use_nt() ? launch_xxh3_pages<MODE, true>(P, pages, n, out, ok, fb, s)
                         : launch_xxh3_pages<MODE, false>(P, pages, n, out, ok, fb, s);
     }

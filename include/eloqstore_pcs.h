@@ -172,12 +172,18 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     default cache policy (0)
  *   PCS_TUNE_XXH64_NT_LOADS       [0] same for the XXH64 page kernels (their
  *                                     64-byte-per-page pieces lose the line's
- *                                     other half under nt: measured slower) */
+ *                                     other half under nt: measured slower)
+ *   PCS_TUNE_STAMP_BYTES        [128] bytes of each page a fixed-size XXH3
+ *                                     stamp rewrites (8, 64, 128 or 256): the
+ *                                     digest plus the unchanged bytes after it;
+ *                                     0 = two passes (digest kernel into a
+ *                                     compact array, then a scatter pass) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
     PCS_TUNE_NT_LOADS = 3,
     PCS_TUNE_XXH64_NT_LOADS = 4,
+    PCS_TUNE_STAMP_BYTES = 5,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Throughput of raw-range XXH3 (long-range kernel) and the manifest API (not part of the product)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import eloqstore_amd as pcs  # noqa: E402
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        torch.cuda._sleep(1_000_000)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+total = 4 << 30
+buf = torch.empty(total, dtype=torch.uint8, device="cuda:0")
+pcs.gen_pages(buf, 4096, total // 4096, 99, 0)
+for chunk in (1 << 20, 64 << 10, 8 << 10):
+    n = total // chunk
+    off = torch.arange(n, dtype=torch.int64, device="cuda:0") * chunk
+    ln = torch.full((n,), chunk, dtype=torch.int32, device="cuda:0")
+    out = torch.empty(n, dtype=torch.int64, device="cuda:0")
+    t = timeit(lambda: pcs.xxh3_64_ranges(buf, off, ln, n, out=out))
+    print(f"raw XXH3 ranges of {chunk >> 10} KiB x {n}: {t*1e3:.3f} ms  {total / t / 1e9:.1f} GB/s", flush=True)
+d_out = torch.empty(1, dtype=torch.int64, device="cuda:0")
+for L in (1 << 20, 64 << 20, 1 << 30, 4 << 30):
+    t = timeit(lambda: pcs._call("pcs_manifest_checksum_dev", buf.data_ptr(), L, d_out.data_ptr(), pcs._stream(None)), 5)
+    print(f"manifest checksum of {L >> 20} MiB: {t*1e3:.3f} ms  {L / t / 1e9:.1f} GB/s", flush=True)

@@ -107,6 +107,26 @@ __global__ __launch_bounds__(256) void k_group16_batchstore(const uint8_t* __res
         }
 }
 
+// A4: group16 nt, non-persistent, with the block -> tile map remapped so the
+// blocks that share an XCD (b % 8 equal) stream one contiguous 1/8 of the
+// buffer (cdna_hip_programming.md T1) instead of interleaving 64 KiB tiles.
+template <int P>
+__global__ __launch_bounds__(256) void k_group16_xcd(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    const uint64_t nb = gridDim.x, b = blockIdx.x;
+    const uint64_t q = nb / 8, tile = (b % 8) * q + b / 8;  // nb % 8 == 0 here
+    const int g = threadIdx.x & 15;
+    const uint64_t pg = tile * 16 + (threadIdx.x >> 4);
+    if (pg >= n) return;
+    const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * P) + g;
+    u32x4 d[P / 256];
+#pragma unroll
+    for (int c = 0; c < P / 256; ++c) d[c] = ld<true>(base + c * 16);
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < P / 256; ++c) r += fold(d[c]);
+    if (r == 0x12345678u) out[pg] = r;
+}
+
 // B: one page per wave, 1 KiB contiguous per wave-instruction
 template <int P, bool NT>
 __global__ __launch_bounds__(256) void k_wavepage(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
@@ -287,6 +307,10 @@ int main(int argc, char** argv) {
     add("batchstore M=64", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 64, false>), dim3(n / 1024), dim3(256), 0, st, pages, n, out); });
     add("batchstore M=16 nt-store", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 16, true>), dim3(n / 256), dim3(256), 0, st, pages, n, out); });
     add("batchstore M=1 nt-store", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 1, true>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
+    add("group16 nt xcd-contiguous tiles", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_xcd<4096>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
+    add("PRODUCT pcs_pages_validate_dev xxh3", [=](hipStream_t st) { pcs_pages_validate_dev(pages, 4096, n, 0, reinterpret_cast<uint8_t*>(out), out + n / 2, (pcs_stream_t)st); });
+    for (int sbytes : {0, 8, 64})
+        add("PRODUCT pcs_pages_stamp_dev xxh3 w=" + std::to_string(sbytes), [=](hipStream_t st) { pcs_set_tuning(PCS_TUNE_STAMP_BYTES, sbytes); pcs_pages_stamp_dev(pages, 4096, n, 0, (pcs_stream_t)st); });
     add("PRODUCT pcs_read_ceiling_dev", [=](hipStream_t st) { pcs_read_ceiling_dev(pages, 4096, n, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh3", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 0, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh64", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 1, out, (pcs_stream_t)st); });
