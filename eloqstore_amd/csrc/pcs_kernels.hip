@@ -903,30 +903,38 @@ __global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pag
     if (i < n) st_nt(reinterpret_cast<uint64_t*>(pages + i * P), dig[i]);
 }
 
-// Same access pattern and output as k_xxh3_fixed<P, kDigest> minus the hash:
-// the achievable HBM read rate for this layout (roofline "measured ceiling").
+// Same loads, tile order and staged result stores as k_xxh3_fixed<P, kDigest>
+// with the hash replaced by an xor/add fold: the achievable rate of this
+// layout (the roofline's "measured ceiling").
 template <int P, bool NT>
 __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
                                                      uint64_t* __restrict__ out) {
-    const int g = threadIdx.x & 15;
+    __shared__ uint64_t tile_r[16];
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 16 + (threadIdx.x >> 4);
-        if (pg >= n) continue;
-        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P) + g;
-        uint32_t x = 0, y = 0, z = 0, w = 0;
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
+        const uint64_t pg = t * 16 + grp;
+        if (pg < n) {
+            const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P) + g;
+            uint32_t x = 0, y = 0, z = 0, w = 0;
 #pragma unroll
-        for (int c = 0; c < P / 256; ++c) {
-            const u32x4 v = ld16<NT>(base + c * 16);
-            x ^= v.x; y += v.y; z ^= v.z; w += v.w;
+            for (int c = 0; c < P / 256; ++c) {
+                const u32x4 v = ld16<NT>(base + c * 16);
+                x ^= v.x; y += v.y; z ^= v.z; w += v.w;
+            }
+            uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + w);
+            r ^= dpp64<kRowRor1>(r);
+            r ^= dpp64<kRowRor2>(r);
+            r ^= dpp64<kRowRor4>(r);
+            r ^= dpp64<kRowRor8>(r);
+            if (g == 0) tile_r[grp] = r;
         }
-        uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + w);
-        r ^= dpp64<kRowRor1>(r);
-        r ^= dpp64<kRowRor2>(r);
-        r ^= dpp64<kRowRor4>(r);
-        r ^= dpp64<kRowRor8>(r);
-        if (g == 0) st_nt(out + pg, r);
+        __syncthreads();
+        const uint64_t i = t * 16 + threadIdx.x;
+        if (threadIdx.x < 16 && i < n) st_nt(out + i, tile_r[threadIdx.x]);
+        __syncthreads();
     }
 }
 
