@@ -137,6 +137,7 @@ TUNE_XXH64_BLOCKS_PER_CU = 2
 TUNE_NT_LOADS = 3
 TUNE_XXH64_NT_LOADS = 4
 TUNE_STAMP_BYTES = 5
+TUNE_XXH64_LAYOUT = 6
 
 
 def set_tuning(key: int, value: int) -> None:

@@ -177,13 +177,18 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     stamp rewrites (8, 64, 128 or 256): the
  *                                     digest plus the unchanged bytes after it;
  *                                     0 = two passes (digest kernel into a
- *                                     compact array, then a scatter pass) */
+ *                                     compact array, then a scatter pass)
+ *   PCS_TUNE_XXH64_LAYOUT         [0] 0 = 16-lane 256 B loads with an LDS hand-
+ *                                     off to the hashing quads (uses
+ *                                     PCS_TUNE_NT_LOADS); 1 = each quad loads
+ *                                     its own 64 B pieces */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
     PCS_TUNE_NT_LOADS = 3,
     PCS_TUNE_XXH64_NT_LOADS = 4,
     PCS_TUNE_STAMP_BYTES = 5,
+    PCS_TUNE_XXH64_LAYOUT = 6,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

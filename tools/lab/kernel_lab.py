@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--bpc", default="1048576,8,32")  # 1048576 = uncapped (one block per 16 pages)
     ap.add_argument("--nt", default="0,1")
     ap.add_argument("--system-hip", action="store_true")
+    ap.add_argument("--x64-layouts", default="0,1")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
     args = ap.parse_args()
     dev = "cuda:0"
@@ -67,17 +68,24 @@ def main():
         for algo_name in args.algos.split(","):
             algo = pcs.XXH3_64 if algo_name == "xxh3" else pcs.XXH64
             key = pcs.TUNE_XXH3_BLOCKS_PER_CU if algo == 0 else pcs.TUNE_XXH64_BLOCKS_PER_CU
-            for bpc in bpcs:
-                for nt in nts:
-                    variants.append((f"{algo_name} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash"))
+            layouts = [int(x) for x in args.x64_layouts.split(",")] if algo == 1 else [0]
+            for lay in layouts:
+                for bpc in bpcs:
+                    for nt in nts:
+                        tag = f" lay={lay}" if algo == 1 else ""
+                        variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash", lay))
         if P in (4096, 65536):
             for nt in nts:
-                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil"))
+                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", 0))
 
         def run(v):
-            _, algo, key, bpc, nt, kind = v
+            _, algo, key, bpc, nt, kind, lay = v
             pcs.set_tuning(key, bpc)
-            pcs.set_tuning(pcs.TUNE_NT_LOADS if algo == 0 else pcs.TUNE_XXH64_NT_LOADS, nt)
+            pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
+            if algo == 1 and lay == 1:
+                pcs.set_tuning(pcs.TUNE_XXH64_NT_LOADS, nt)
+            else:
+                pcs.set_tuning(pcs.TUNE_NT_LOADS, nt)
             if kind == "ceil":
                 pcs.read_ceiling(pages, P, n, out)
             elif P is None:
@@ -118,6 +126,7 @@ def main():
     pcs.set_tuning(pcs.TUNE_XXH64_BLOCKS_PER_CU, 0)
     pcs.set_tuning(pcs.TUNE_NT_LOADS, 1)
     pcs.set_tuning(pcs.TUNE_XXH64_NT_LOADS, 0)
+    pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, 0)
 
 
 if __name__ == "__main__":
