@@ -57,6 +57,8 @@ _SIGS = {
     "pcs_gen_desc_dev": [_vp, _vp, _vp, _u64, _u64, _u64, _vp],
     "pcs_flip_byte_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
     "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
+    "pcs_host_alloc_pinned": [_u64, _P(_vp)],
+    "pcs_host_free_pinned": [_vp],
     "pcs_batch_create": [_P(_vp)],
     "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32],
     "pcs_batch_poll": [_vp],

@@ -11,6 +11,8 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <thread>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -142,6 +144,51 @@ struct HostCtx {
 
 thread_local std::unordered_map<int, HostCtx> t_ctx;
 
+// True when pages[0..n) are one contiguous run in pinned host memory.
+bool contiguous_pinned(const void* const* pages, uint64_t n, uint64_t P) {
+    if (n == 0) return false;
+    const uint8_t* base = static_cast<const uint8_t*>(pages[0]);
+    for (uint64_t i = 1; i < n; ++i)
+        if (pages[i] != base + i * P) return false;
+    hipPointerAttribute_t attr{};
+    const bool pinned = hipPointerGetAttributes(&attr, base) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return pinned;
+}
+
+// Gather scattered host pages into pinned staging.  Large chunks are split
+// over several threads: one thread's memcpy from pageable memory (~14 GiB/s
+// measured) is well below PCIe Gen5, so the host-fed path was gather-bound.
+// PCS_GATHER_THREADS overrides the thread count (1 = serial).
+unsigned gather_threads() {
+    static const unsigned k = [] {
+        if (const char* e = std::getenv("PCS_GATHER_THREADS")) {
+            const long v = std::strtol(e, nullptr, 10);
+            if (v >= 1 && v <= 64) return (unsigned)v;
+        }
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        return std::min(8u, std::max(1u, hw / 2));
+    }();
+    return k;
+}
+
+void gather(uint8_t* dst, const void* const* pages, uint64_t first, uint64_t cnt, uint64_t P) {
+    const uint64_t bytes = cnt * P;
+    const unsigned T = bytes >= (8u << 20) ? gather_threads() : 1;
+    auto run = [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; ++i) std::memcpy(dst + i * P, pages[first + i], P);
+    };
+    if (T <= 1) {
+        run(0, cnt);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (unsigned k = 1; k < T; ++k) th.emplace_back(run, cnt * k / T, cnt * (k + 1) / T);
+    run(0, cnt / T);
+    for (auto& x : th) x.join();
+}
+
 int ensure_slot(Slot& s, size_t page_bytes, size_t n) {
     hipError_t e;
     if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
@@ -198,14 +245,8 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
     const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, kStageBytes / P));
     // Pages that are one contiguous, pinned (hipHostMalloc'd / hipHostRegister'ed)
     // run are DMA'd straight from the caller's memory: no gather copy.
-    bool direct = true;
     const uint8_t* base = static_cast<const uint8_t*>(pages[0]);
-    for (uint64_t i = 1; i < n && direct; ++i) direct = pages[i] == base + i * P;
-    if (direct) {
-        hipPointerAttribute_t attr{};
-        direct = hipPointerGetAttributes(&attr, base) == hipSuccess && attr.type == hipMemoryTypeHost;
-        (void)hipGetLastError();
-    }
+    const bool direct = contiguous_pinned(pages, n, P);
     for (auto& s : ctx.slot)
         if (int rc = ensure_slot(s, direct ? 0 : chunk * P, chunk)) return rc;
     if (direct)  // device page buffers are still needed per slot
@@ -245,8 +286,7 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
         Slot& s = ctx.slot[k % kSlots];
         if ((rc = drain(s))) break;
         const uint64_t cnt = std::min(chunk, n - first);
-        if (!direct)
-            for (uint64_t i = 0; i < cnt; ++i) std::memcpy(s.h_pages + i * P, pages[first + i], P);
+        if (!direct) gather(s.h_pages, pages, first, cnt, P);
         s.first = first;
         s.count = cnt;
         e = hipMemcpyAsync(s.d_pages, direct ? base + first * P : s.h_pages, cnt * P, hipMemcpyHostToDevice,
@@ -418,6 +458,22 @@ int pcs_pages_digest_host(const void* const* pages, uint64_t page_size, uint64_t
     return host_batch(0, pages, page_size, n_pages, algo, nullptr, nullptr, digests);
 }
 
+int pcs_host_alloc_pinned(uint64_t bytes, void** out) {
+    if (!out) return fail(PCS_ERR_INVALID, "out is null");
+    *out = nullptr;
+    if (int rc = require_device()) return rc;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return fail(PCS_ERR_NOMEM, "hipHostMalloc failed");
+    }
+    return PCS_OK;
+}
+
+int pcs_host_free_pinned(void* p) {
+    if (!p) return PCS_OK;
+    return finish(hipHostFree(p), "hipHostFree");
+}
+
 int pcs_batch_create(pcs_batch** out) {
     if (!out) return fail(PCS_ERR_INVALID, "out is null");
     *out = nullptr;
@@ -482,9 +538,10 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
         b->first_bad = UINT64_MAX;
         return PCS_OK;
     }
-    for (uint64_t i = 0; i < n; ++i) std::memcpy(b->h_pages + i * P, pages[i], P);
+    const bool direct = contiguous_pinned(pages, n, P);
+    if (!direct) gather(b->h_pages, pages, 0, n, P);
     hipStream_t s = b->stream;
-    e = hipMemcpyAsync(b->d_pages, b->h_pages, n * P, hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(b->d_pages, direct ? pages[0] : b->h_pages, n * P, hipMemcpyHostToDevice, s);
     const int kmode = mode == PCS_BATCH_VALIDATE ? 1 : 0;
     if (e == hipSuccess) e = pcs::run_pages(kmode, algo, b->d_pages, P, n, b->d_dig, b->d_ok, nullptr, s);
     if (e == hipErrorNotSupported) {

@@ -121,13 +121,20 @@ int pcs_pages_stamp_host(void *const *pages, uint64_t page_size, uint64_t n_page
 int pcs_pages_digest_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
                           int algo, uint64_t *digests);
 
+/* Pinned (page-locked) host memory, e.g. for an io_uring buffer ring or file
+ * staging: batches over one contiguous pinned run are DMA'd with no gather. */
+int pcs_host_alloc_pinned(uint64_t bytes, void **out);
+int pcs_host_free_pinned(void *p);
+
 /* ---- asynchronous host batches (shard-loop integration) --------------------
  * EloqStore's shard thread never blocks: its work loop is Submit() ->
  * PollComplete() -> ExecuteReadyTasks() (src/storage/shard.cpp:67-130), and
  * a ReadPages / FlushBatchPages coroutine yields while I/O is in flight.  A
  * pcs_batch is the checksum analogue: submit gathers the pages (or DMAs a
  * pinned contiguous run directly), enqueues H2D + kernel + D2H on the batch's
- * own stream and returns; poll answers "done?" without blocking.  One batch
+ * own stream and returns; poll answers "done?" without blocking.  A batch
+ * whose pages are one contiguous pinned run is DMA'd in place (the caller
+ * must then not modify the pages until completion).  One batch
  * object holds one batch in flight; create several for more concurrency.
  * Pages must stay valid until the batch completes (stamp writes the digests
  * into them when poll/wait observes completion). */

@@ -293,6 +293,13 @@ def test_cli(tmp_path):
     assert r.returncode == 2 and r.stdout.startswith("Checksum FAILED for page at offset 20480")
     r = subprocess.run([tool, "--scan", str(f)], capture_output=True, text=True)
     assert r.returncode == 2 and "64 pages of 4096 bytes: 1 corrupted, first at offset 20480" in r.stdout
+    r = subprocess.run([tool, "--stamp", str(f)], capture_output=True, text=True)
+    assert r.returncode == 0 and "Stamped 64 pages" in r.stdout
+    r = subprocess.run([tool, "--scan", str(f)], capture_output=True, text=True)
+    assert r.returncode == 0 and "64 pages of 4096 bytes: 0 corrupted" in r.stdout
+    raw = np.fromfile(f, dtype=np.uint8)
+    assert np.array_equal(raw.reshape(64, 4096)[:, :8].copy().view(np.uint64).reshape(-1),
+                          oracle.pages_digest(raw, 4096))
     r = subprocess.run([tool, str(f), "0", "0"], capture_output=True, text=True)
     assert r.returncode == 1 and "Invalid page size" in r.stderr
     r = subprocess.run([tool, str(f), "262141"], capture_output=True, text=True)
@@ -454,3 +461,50 @@ def test_cpp_dropin_program():
     exe = os.path.join(os.path.dirname(__file__), "cpp", "dropin_test")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "dropin ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+@pytest.mark.parametrize("shift", [1, 8, 24])
+def test_unaligned_page_base(algo, shift):
+    """Pages whose base is not 16-byte aligned take the descriptor fallback;
+    results must not change."""
+    P, n = 4096, 37
+    buf = dev_pages(P, n, 0x5EED00C0, 0, extra=64)
+    host = buf.cpu().numpy()
+    shifted = torch.empty(n * P + 64, dtype=torch.uint8, device=DEV)
+    shifted[shift:shift + n * P] = buf[: n * P]
+    got = u64(pcs.pages_digest(shifted[shift:], P, n, algo))
+    assert np.array_equal(got, oracle.pages_digest(host[: n * P], P, algo))
+    pcs.pages_stamp(shifted[shift:], P, n, algo)
+    ok, fb = pcs.pages_validate(shifted[shift:], P, n, algo)
+    assert int(ok.sum()) == n
+
+
+def test_host_api_concurrent_threads():
+    """Host batches from several threads at once (each thread owns its staging
+    and streams; ctypes drops the GIL during the call)."""
+    import threading
+
+    P = 4096
+    errors = []
+
+    def worker(tid):
+        try:
+            pages = [bytearray(splitmix_words(700 + tid, i, P // 8).tobytes()) for i in range(300)]
+            for _ in range(3):
+                pcs.set_checksums(pages, P)
+                ok, fb = pcs.validate_checksums(pages, P)
+                assert all(ok) and fb is None
+                pages[tid * 7][100] ^= 1
+                ok, fb = pcs.validate_checksums(pages, P)
+                assert fb == tid * 7
+                pages[tid * 7][100] ^= 1
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
