@@ -116,17 +116,48 @@ class Workload:
             self.d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
             pcs.gen_desc(self.pages, self.d_off, self.d_len, self.n, seed, self.first)
             self.out = torch.empty(self.n, dtype=torch.int64, device=dev)
+        self.ok = torch.empty(self.n, dtype=torch.uint8, device=dev)
+        self.fb = torch.empty(1, dtype=torch.int64, device=dev)
         torch.cuda.synchronize()
 
-    def step(self):
+    def step(self, mode: str = "digest"):
         if self.P is not None:
-            pcs.pages_digest(self.pages, self.P, self.n, self.algo, out=self.out)
+            if mode == "digest":
+                pcs.pages_digest(self.pages, self.P, self.n, self.algo, out=self.out)
+            elif mode == "validate":
+                pcs.pages_validate(self.pages, self.P, self.n, self.algo, ok=self.ok, first_bad=self.fb)
+            else:
+                pcs.pages_stamp(self.pages, self.P, self.n, self.algo)
         else:
-            pcs.desc_digest(self.pages, self.d_off, self.d_len, self.n, self.algo, out=self.out)
+            if mode == "digest":
+                pcs.desc_digest(self.pages, self.d_off, self.d_len, self.n, self.algo, out=self.out)
+            elif mode == "validate":
+                pcs.desc_validate(self.pages, self.d_off, self.d_len, self.n, self.algo, ok=self.ok, first_bad=self.fb)
+            else:
+                pcs.desc_stamp(self.pages, self.d_off, self.d_len, self.n, self.algo)
 
-    def algorithmic_bytes(self) -> int:
-        # every page byte read once (the 8-byte header shares the first line) + 8 B digest written
-        return self.bytes + 8 * self.n
+    def corruption_drill(self, every: int = 1000):
+        """Untimed self-check (persist.cpp:241-246 style): stamp every page,
+        validate (all pass), flip byte 10 of every `every`-th page, validate:
+        exactly those must fail and the first bad index must be 0."""
+        if self.P is None:
+            return None
+        pcs.pages_stamp(self.pages, self.P, self.n, self.algo)
+        pcs.pages_validate(self.pages, self.P, self.n, self.algo, ok=self.ok, first_bad=self.fb)
+        clean = int(self.ok.sum().item())
+        pcs.flip_byte(self.pages, self.P, self.n, every=every, byte_offset=10)
+        pcs.pages_validate(self.pages, self.P, self.n, self.algo, ok=self.ok, first_bad=self.fb)
+        flipped = (self.n + every - 1) // every
+        detected = int((self.ok == 0).sum().item())
+        first = int(self.fb.item())
+        pcs.flip_byte(self.pages, self.P, self.n, every=every, byte_offset=10)  # restore
+        return {"pages": self.n, "valid_after_stamp": clean, "flipped": flipped, "detected": detected,
+                "first_bad": first, "pass": clean == self.n and detected == flipped and first == 0}
+
+    def algorithmic_bytes(self, mode: str = "digest") -> int:
+        # every page byte read once (the 8-byte header shares the first line) + the result written:
+        # 8 B digest (digest), 1 B verdict (validate), 8 B into the page (stamp)
+        return self.bytes + (1 if mode == "validate" else 8) * self.n
 
     def read_ceiling(self, reps: int) -> float | None:
         if self.P is None or self.P not in (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
@@ -195,6 +226,48 @@ def cpu_baseline(w: Workload, target_s: float):
         {"pages": int(host.nbytes // P), "mismatches": int((want != gpu).sum())}
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_all_cores(w: Workload, target_s: float):
+    """The same reference loop on several host threads (disjoint page ranges of
+    the sample), for context: BASELINE.md's all-cores CPU figure."""
+    import threading
+
+    import oracle  # baseline infrastructure only
+
+    if w.P is None or oracle.ref_lib() is None:
+        return None
+    host, P, _ = w.sample_pages_host(256 << 20)
+    k = host.nbytes // P
+    nthreads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    parts = [host[i * k // nthreads * P:(i + 1) * k // nthreads * P] for i in range(nthreads)]
+    done = [0] * nthreads
+    stop = time.perf_counter() + target_s
+
+    def run(i):
+        while time.perf_counter() < stop:
+            oracle.ref_pages_digest(parts[i], P, w.algo)
+            done[i] += parts[i].nbytes
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=run, args=(i,)) for i in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"value": round(sum(done) / dt / GIB, 2), "unit": "GiB/s", "cores": nthreads, "kind": "reference",
+            "cpu": cpu_model(), "sample": f"{k} pages split over {nthreads} threads, ~{target_s:.0f} s"}
+
+
 def host_inclusive(w: Workload, max_pages: int = 1 << 18):
     """Pages starting in host memory: H2D + kernel + D2H of digests, through
     pcs_pages_digest_host.  (a) one contiguous pinned run -> direct DMA;
@@ -248,6 +321,9 @@ def main():
     ap.add_argument("--pages-per-gpu", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["digest", "validate", "stamp"], default="digest",
+                    help="digest (metric), validate (read path), stamp (write path)")
+    ap.add_argument("--all-cores", action="store_true", help="also time the CPU reference on all host threads")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the host-memory path (pinned direct DMA and pageable gather)")
     args = ap.parse_args()
@@ -265,9 +341,12 @@ def main():
     algo = pcs.XXH3_64 if args.algo == "xxh3" else pcs.XXH64
 
     w = Workload(args.config, algo, rank, args.pages_per_gpu, dev)
+    if args.mode == "validate":  # the read path checks stamped pages (mostly valid)
+        w.step("stamp")
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        w.step()
+        w.step(args.mode)
     torch.cuda.synchronize()
 
     # per-launch HIP events on the launch stream (torch's current stream)
@@ -278,7 +357,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record()
-        w.step()
+        w.step(args.mode)
         ends[i].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -289,15 +368,23 @@ def main():
     total_bytes = sum_over_ranks(dist, float(w.bytes)) * args.steps
     value = total_bytes / elapsed / GIB
 
+    if args.mode != "digest":  # leave self.out holding this batch's digests for the parity leg
+        w.step("digest")
+        torch.cuda.synchronize()
     ceiling = w.read_ceiling(max(3, args.steps // 5))
-    cpu, parity = (None, None)
+    cpu, parity, allcores = (None, None, None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(w, args.cpu_seconds)
+        if cpu is not None:
+            cpu["cpu"] = cpu_model()
+        if args.all_cores:
+            allcores = cpu_all_cores(w, min(args.cpu_seconds, 5.0))
+    drill = w.corruption_drill() if rank == 0 else None
     hostinc = host_inclusive(w) if args.host_inclusive and rank == 0 else None
 
     if rank == 0:
-        achieved = w.algorithmic_bytes() / avg_launch / 1e9
-        traffic = committed_traffic(args.config, algo)
+        achieved = w.algorithmic_bytes(args.mode) / avg_launch / 1e9
+        traffic = committed_traffic(args.config, algo) if args.mode == "digest" else None
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -317,7 +404,7 @@ def main():
                 "pages_per_gpu": w.n,
                 "bytes_per_gpu": w.bytes,
                 "algo": "xxh3_64" if algo == 0 else "xxh64",
-                "mode": "digest (pcs_pages_digest_dev)" if w.P else "digest (pcs_desc_digest_dev)",
+                "mode": f"{args.mode} ({'pcs_pages' if w.P else 'pcs_desc'}_{args.mode}_dev)",
                 "parallelism": f"page shards x{world}, no collective",
             },
             "roofline": {
@@ -328,7 +415,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
-                "algorithmic_bytes_per_launch": w.algorithmic_bytes(),
+                "algorithmic_bytes_per_launch": w.algorithmic_bytes(args.mode),
                 "avg_launch_ms": round(avg_launch * 1e3, 4),
                 "min_launch_ms": round(launch_s[0] * 1e3, 4),
             },
@@ -336,6 +423,9 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        line["corruption_drill"] = drill
+        if allcores is not None:
+            line["cpu_all_cores"] = allcores
         if hostinc is not None:
             line["host_inclusive"] = hostinc
         print(json.dumps(line), flush=True)

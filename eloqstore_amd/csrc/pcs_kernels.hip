@@ -75,6 +75,15 @@ __device__ __forceinline__ uint64_t hi64(u32x4 v) { return ((uint64_t)v.w << 32)
 template <typename T>
 __device__ __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
 
+// first_bad = min(first_bad, idx).  The word only ever decreases, so a stale
+// (larger) read can only cause an unneeded atomic, never skip a needed one;
+// reading first keeps a batch of mostly corrupt pages from serialising on
+// one address.
+__device__ __forceinline__ void note_bad(unsigned long long* first_bad, uint64_t idx) {
+    if ((unsigned long long)idx < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(first_bad, (unsigned long long)idx);
+}
+
 __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_t stored, uint8_t* page_w,
                                      uint64_t* out, uint8_t* ok, unsigned long long* first_bad) {
     if (mode == kStamp) {
@@ -84,7 +93,7 @@ __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_
         const bool good = (h == stored);
         st_nt(ok + idx, (uint8_t)(good ? 1 : 0));
         if (out) st_nt(out + idx, h);
-        if (!good && first_bad) atomicMin(first_bad, (unsigned long long)idx);
+        if (!good && first_bad) note_bad(first_bad, idx);
     } else {
         st_nt(out + idx, h);
     }
@@ -326,7 +335,6 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
             } else if (L.g == 0) {
                 tile_h[grp] = h;
                 tile_ok[grp] = (h == stored) ? 1 : 0;
-                if (MODE == kValidate && h != stored && first_bad) atomicMin(first_bad, (unsigned long long)pg);
             }
         }
         if (MODE != kStamp) {
@@ -335,6 +343,14 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
             if (threadIdx.x < 16 && i < n) {
                 if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
                 if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
+            }
+            if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+                // one note per tile: its smallest failing page
+                for (int k = 0; k < 16 && t * 16 + k < n; ++k)
+                    if (!tile_ok[k]) {
+                        note_bad(first_bad, t * 16 + k);
+                        break;
+                    }
             }
             __syncthreads();
         }
@@ -850,7 +866,7 @@ __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict_
             if (MODE == kValidate) {
                 ok[i] = 0;
                 if (out) out[i] = 0;
-                if (first_bad) atomicMin(first_bad, (unsigned long long)i);
+                if (first_bad) note_bad(first_bad, i);
             } else if (MODE == kDigest) {
                 out[i] = 0;
             }
