@@ -27,6 +27,7 @@ Also reported, on the same line:
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -293,7 +294,63 @@ def host_inclusive(w: Workload, max_pages: int = 1 << 18):
         dt = (time.perf_counter() - t0) / reps
         res[f"{name}_GiBps"] = round(nbytes / dt / GIB, 2)
         res[f"{name}_digests_match_device"] = bool(np.array_equal(digests, w.out[:k].cpu().numpy().view(np.uint64)))
+    # Scattered pool pages (a random permutation, like pages spread over
+    # PagesPool chunks): (c) unregistered -> gather; (d) registered pool ->
+    # zero-copy, one launch reading the pages in place.
+    perm = np.random.default_rng(7).permutation(k).astype(np.uint64)
+    want = w.out[:k].cpu().numpy().view(np.uint64)[perm]
+    with pcs.PagePool(k, w.P) as pool:
+        pool.pages.reshape(-1)[:] = pageable
+        for name, base in (("gather_scattered", pageable.ctypes.data), ("zero_copy_scattered", pool.base)):
+            ptrs = perm * np.uint64(w.P) + np.uint64(base)
+            fn = pcs.lib().pcs_pages_digest_host
+            rc = fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)
+            assert rc == 0, pcs.lib().pcs_last_error()
+            reps, t0 = 0, time.perf_counter()
+            while reps < 3 or time.perf_counter() - t0 < 2.0:
+                fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)
+                reps += 1
+            dt = (time.perf_counter() - t0) / reps
+            res[f"{name}_GiBps"] = round(nbytes / dt / GIB, 2)
+            res[f"{name}_digests_match_device"] = bool(np.array_equal(digests, want))
+        res["batch_latency_us"] = batch_latency(pool, pageable, w)
     return res
+
+
+def batch_latency(pool, pageable, w: Workload):
+    """Median wall time of one validate call over a read-path-sized batch
+    (max_read_pages_batch = 128, kv_options.h:18-19; write batches <= 256),
+    scattered pages: staged (gather) vs zero-copy (registered pool), and the
+    async form (submit + poll spin) on the registered pool."""
+    out = {}
+    rng = np.random.default_rng(11)
+    for nb in (1, 16, 128, 256):
+        idx = rng.permutation(pool.n)[:nb].astype(np.uint64)
+        row = {}
+        for name, base in (("gather", pageable.ctypes.data), ("zero_copy", pool.base)):
+            ptrs = idx * np.uint64(w.P) + np.uint64(base)
+            ok = np.empty(nb, dtype=np.uint8)
+            fb = ctypes.c_uint64()
+            fn = pcs.lib().pcs_pages_validate_host
+            ts = []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                fn(ptrs.ctypes.data, w.P, nb, w.algo, ok.ctypes.data, ctypes.byref(fb))
+                ts.append(time.perf_counter() - t0)
+            row[name] = round(float(np.median(ts[20:])) * 1e6, 1)
+        b = pcs.Batch()
+        ptrs = idx * np.uint64(w.P) + np.uint64(pool.base)
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            b.submit_ptrs(pcs.Batch.VALIDATE, ptrs, w.P, w.algo)
+            while not b.poll():
+                pass
+            ts.append(time.perf_counter() - t0)
+        b.close()
+        row["zero_copy_async"] = round(float(np.median(ts[20:])) * 1e6, 1)
+        out[str(nb)] = row
+    return out
 
 
 def committed_traffic(cfg: int, algo: int):

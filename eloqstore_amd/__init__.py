@@ -17,6 +17,8 @@ import ctypes
 import os
 import re
 
+import numpy as np
+
 import torch  # noqa: F401  (loads the process's HIP runtime before the library)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -59,6 +61,8 @@ _SIGS = {
     "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
     "pcs_host_alloc_pinned": [_u64, _P(_vp)],
     "pcs_host_free_pinned": [_vp],
+    "pcs_host_register": [_vp, _u64],
+    "pcs_host_unregister": [_vp],
     "pcs_batch_create": [_P(_vp)],
     "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32],
     "pcs_batch_poll": [_vp],
@@ -70,11 +74,12 @@ _SIGS = {
     "pcs_manifest_validate_host": [_vp, _u64, _P(_i32)],
     "pcs_set_tuning": [_i32, ctypes.c_int64],
     "pcs_get_tuning": [_i32],
+    "pcs_counter": [_i32],
     "pcs_version": [],
     "pcs_last_error": [],
 }
 _STR = {"pcs_version", "pcs_last_error"}
-_I64 = {"pcs_get_tuning"}
+_I64 = {"pcs_get_tuning", "pcs_counter"}
 
 
 class PcsError(RuntimeError):
@@ -140,6 +145,16 @@ TUNE_NT_LOADS = 3
 TUNE_XXH64_NT_LOADS = 4
 TUNE_STAMP_BYTES = 5
 TUNE_XXH64_LAYOUT = 6
+TUNE_ZERO_COPY = 7
+
+COUNTER_ZERO_COPY_LAUNCHES = 0
+COUNTER_DIRECT_DMA_CHUNKS = 1
+COUNTER_GATHER_CHUNKS = 2
+
+
+def counter(which: int) -> int:
+    """pcs_counter: how host batches were served (process-wide, monotonic)."""
+    return int(lib().pcs_counter(which))
 
 
 def set_tuning(key: int, value: int) -> None:
@@ -273,6 +288,14 @@ class Batch:
         self.mode = mode
         _call("pcs_batch_submit", self._b, mode, arr, page_size, len(pages), algo)
 
+    def submit_ptrs(self, mode: int, ptrs, page_size: int, algo: int = XXH3_64) -> None:
+        """Submit raw page addresses (a uint64 array of host pointers)."""
+        ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        self._keep = ptrs
+        self.n = len(ptrs)
+        self.mode = mode
+        _call("pcs_batch_submit", self._b, mode, ptrs.ctypes.data, page_size, len(ptrs), algo)
+
     def poll(self) -> bool:
         rc = lib().pcs_batch_poll(self._b)
         if rc < 0:
@@ -346,3 +369,73 @@ def page_digests_host(pages: list, page_size: int, algo: int = XXH3_64) -> list:
     out = (ctypes.c_uint64 * len(pages))()
     _call("pcs_pages_digest_host", arr, page_size, len(pages), algo, out)
     return list(out)
+
+
+# ---- raw pointer arrays and registered page pools -----------------------------
+
+def host_register(addr: int, nbytes: int) -> None:
+    """pcs_host_register: page-lock + map a host region for zero-copy batches."""
+    _call("pcs_host_register", addr, nbytes)
+
+
+def host_unregister(addr: int) -> None:
+    _call("pcs_host_unregister", addr)
+
+
+def validate_ptrs(ptrs, page_size: int, algo: int = XXH3_64):
+    """pcs_pages_validate_host over raw host page addresses -> (ok array, first_bad or None)."""
+    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    ok = np.zeros(max(1, len(ptrs)), dtype=np.uint8)
+    fb = ctypes.c_uint64(0)
+    _call("pcs_pages_validate_host", ptrs.ctypes.data, page_size, len(ptrs), algo, ok.ctypes.data, ctypes.byref(fb))
+    return ok[: len(ptrs)], (None if fb.value == (1 << 64) - 1 else fb.value)
+
+
+def stamp_ptrs(ptrs, page_size: int, algo: int = XXH3_64) -> None:
+    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    _call("pcs_pages_stamp_host", ptrs.ctypes.data, page_size, len(ptrs), algo)
+
+
+def digest_ptrs(ptrs, page_size: int, algo: int = XXH3_64) -> np.ndarray:
+    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    out = np.zeros(max(1, len(ptrs)), dtype=np.uint64)
+    _call("pcs_pages_digest_host", ptrs.ctypes.data, page_size, len(ptrs), algo, out.ctypes.data)
+    return out[: len(ptrs)]
+
+
+class PagePool:
+    """A page-aligned host region of n_pages x page_size, like one chunk of
+    EloqStore's PagesPool (page.cpp:95-120), registered for zero-copy batches.
+    `.pages` is a (n_pages, page_size) uint8 view; `.ptr(i)` a page address."""
+
+    def __init__(self, n_pages: int, page_size: int, register: bool = True):
+        import mmap
+        self.n, self.P = n_pages, page_size
+        self._map = mmap.mmap(-1, max(1, n_pages * page_size))
+        self.pages = np.frombuffer(self._map, dtype=np.uint8)[: n_pages * page_size].reshape(n_pages, page_size)
+        self.base = self.pages.ctypes.data
+        self.registered = False
+        if register:
+            host_register(self.base, n_pages * page_size)
+            self.registered = True
+
+    def ptr(self, i) -> np.ndarray:
+        return np.uint64(self.base) + np.asarray(i, dtype=np.uint64) * np.uint64(self.P)
+
+    def close(self) -> None:
+        if self.registered:
+            host_unregister(self.base)
+            self.registered = False
+        self.pages = None
+        if self._map is not None:
+            try:
+                self._map.close()
+            except BufferError:  # a view is still alive; let GC unmap it
+                pass
+            self._map = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

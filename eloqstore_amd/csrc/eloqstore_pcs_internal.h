@@ -20,6 +20,17 @@ hipError_t run_desc(int mode, int algo, const uint8_t* base, const uint64_t* off
                     int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* first_bad,
                     hipStream_t s);
 
+// Page list: page i is the absolute device-visible address ptrs[i] (pool
+// pages in registered host memory), all of size page_size.  ptrs, out and ok
+// may live in pinned host memory.  No first_bad word: the caller scans the
+// verdicts.  Only the fast shapes (list_shape_ok) are supported.
+inline bool list_shape_ok(int algo, uint64_t P) {
+    return algo == 0 ? (P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull)
+                     : (P % 64 == 0 && P >= 128 && P <= 0xFFFFFFFFull);
+}
+hipError_t run_list(int mode, int algo, const uint64_t* ptrs, uint64_t page_size, uint64_t n, uint64_t* out,
+                    uint8_t* ok, hipStream_t s);
+
 hipError_t run_gen_pages(uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t seed, uint64_t first_page,
                          hipStream_t s);
 hipError_t run_gen_desc(uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n, uint64_t seed,

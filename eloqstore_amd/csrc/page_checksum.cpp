@@ -59,6 +59,14 @@ void PageDigests(std::span<const char* const> pages, size_t page_size, uint64_t*
         die("PageDigests", rc);
 }
 
+void RegisterPagePool(void* base, size_t bytes) {
+    if (int rc = pcs_host_register(base, bytes)) die("RegisterPagePool", rc);
+}
+
+void UnregisterPagePool(void* base) {
+    if (int rc = pcs_host_unregister(base)) die("UnregisterPagePool", rc);
+}
+
 ChecksumBatch::ChecksumBatch() {
     if (int rc = pcs_batch_create(&batch_)) die("ChecksumBatch", rc);
 }

@@ -10,11 +10,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
-#include <thread>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -107,6 +111,112 @@ int desc_common(int mode, const void* d_base, const uint64_t* d_off, const uint3
 }
 
 // ---------------------------------------------------------------------------
+// registered host regions (zero-copy page pools)
+// ---------------------------------------------------------------------------
+struct Region {
+    uint64_t bytes;
+    uintptr_t dev;  // device-visible address of the region base
+    bool allocated; // pcs_host_alloc_pinned (freed there, not unregistered)
+};
+std::shared_mutex g_reg_mu;
+std::map<uintptr_t, Region> g_regions;  // keyed by host base address
+
+int add_region(void* p, uint64_t bytes, bool allocated) {
+    void* dev = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dev, p, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+    std::unique_lock lk(g_reg_mu);
+    const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+    auto it = g_regions.upper_bound(b);
+    if (it != g_regions.end() && it->first < b + bytes) return fail(PCS_ERR_INVALID, "region overlaps a registered one");
+    if (it != g_regions.begin()) {
+        auto pv = std::prev(it);
+        if (pv->first + pv->second.bytes > b) return fail(PCS_ERR_INVALID, "region overlaps a registered one");
+    }
+    g_regions.emplace(b, Region{bytes, reinterpret_cast<uintptr_t>(dev), allocated});
+    return PCS_OK;
+}
+
+// Device-visible addresses of pages[0..n) when every page [p, p + P) lies in a
+// registered region and is 16-byte aligned; false otherwise.
+bool translate_registered(const void* const* pages, uint64_t n, uint64_t P, uint64_t* dev_out) {
+    std::shared_lock lk(g_reg_mu);
+    if (g_regions.empty()) return false;
+    auto hint = g_regions.end();
+    for (uint64_t i = 0; i < n; ++i) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(pages[i]);
+        if (a % 16) return false;
+        if (hint == g_regions.end() || a < hint->first || a + P > hint->first + hint->second.bytes) {
+            auto it = g_regions.upper_bound(a);
+            if (it == g_regions.begin()) return false;
+            hint = std::prev(it);
+            if (a + P > hint->first + hint->second.bytes) return false;
+        }
+        dev_out[i] = hint->second.dev + (a - hint->first);
+    }
+    return true;
+}
+
+template <typename T>
+T* dev_alias(T* host_pinned) {
+    void* d = nullptr;
+    return hipHostGetDevicePointer(&d, host_pinned, 0) == hipSuccess ? static_cast<T*>(d) : nullptr;
+}
+
+// Pinned, device-mapped result buffers of one zero-copy launch.
+struct ZcBufs {
+    uint64_t* h_ptrs = nullptr;
+    uint64_t* h_dig = nullptr;
+    uint8_t* h_ok = nullptr;
+    uint64_t* d_ptrs = nullptr;  // device aliases of the above
+    uint64_t* d_dig = nullptr;
+    uint8_t* d_ok = nullptr;
+    size_t cap = 0;
+    void release() {
+        (void)hipHostFree(h_ptrs);
+        (void)hipHostFree(h_dig);
+        (void)hipHostFree(h_ok);
+        *this = ZcBufs{};
+    }
+    int ensure(size_t n) {
+        if (n <= cap) return PCS_OK;
+        release();
+        if (hipHostMalloc(reinterpret_cast<void**>(&h_ptrs), n * 8, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&h_ok), n, hipHostMallocDefault) != hipSuccess) {
+            release();
+            return fail(PCS_ERR_NOMEM, "zero-copy buffer allocation failed");
+        }
+        d_ptrs = dev_alias(h_ptrs);
+        d_dig = dev_alias(h_dig);
+        d_ok = dev_alias(h_ok);
+        if (!d_ptrs || !d_dig || !d_ok) {
+            release();
+            return fail(PCS_ERR_HIP, "hipHostGetDevicePointer failed for zero-copy buffers");
+        }
+        cap = n;
+        return PCS_OK;
+    }
+};
+
+std::atomic<uint64_t> g_counters[3];
+void count(int which) { g_counters[which].fetch_add(1, std::memory_order_relaxed); }
+
+int64_t zero_copy_policy() { return pcs::get_tuning(PCS_TUNE_ZERO_COPY); }
+
+// Zero-copy eligibility for a host batch: fast shape, policy, and every page
+// registered (fills zc.h_ptrs with device-visible page addresses).
+bool zero_copy_eligible(ZcBufs& zc, const void* const* pages, uint64_t n, uint64_t P, int algo) {
+    const int64_t pol = zero_copy_policy();
+    if (pol == 0 || n == 0 || !pcs::list_shape_ok(algo, P)) return false;
+    if (zc.ensure(n) != PCS_OK) {
+        (void)hipGetLastError();
+        return false;  // staging path still works
+    }
+    return translate_registered(pages, n, P, zc.h_ptrs);
+}
+
+// ---------------------------------------------------------------------------
 // host-memory pipeline
 // ---------------------------------------------------------------------------
 constexpr size_t kStageBytes = 32u << 20;  // per slot
@@ -128,7 +238,10 @@ constexpr int kSlots = 3;  // H2D of chunk k+1 || kernel k || D2H k-1
 
 struct HostCtx {
     Slot slot[kSlots];
+    ZcBufs zc;
     ~HostCtx() {
+        if (slot[0].stream) (void)hipStreamSynchronize(slot[0].stream);
+        zc.release();
         for (auto& s : slot) {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
             (void)hipHostFree(s.h_pages);
@@ -245,6 +358,29 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
     const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, kStageBytes / P));
     // Pages that are one contiguous, pinned (hipHostMalloc'd / hipHostRegister'ed)
     // run are DMA'd straight from the caller's memory: no gather copy.
+    if (zero_copy_eligible(ctx.zc, pages, n, P, algo)) {
+        // Registered pages: one launch reads them in place and writes the
+        // verdicts / digests / page headers straight to host memory.
+        if (int rc = ensure_slot(ctx.slot[0], 0, 1)) return rc;
+        hipStream_t zs = ctx.slot[0].stream;
+        e = pcs::run_list(mode, algo, ctx.zc.d_ptrs, P, n, mode == 0 ? ctx.zc.d_dig : nullptr,
+                          mode == 1 ? ctx.zc.d_ok : nullptr, zs);
+        if (e == hipSuccess) e = hipStreamSynchronize(zs);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy page list");
+        count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
+        if (mode == 1) {
+            std::memcpy(out_ok, ctx.zc.h_ok, n);
+            if (first_bad)
+                for (uint64_t i = 0; i < n; ++i)
+                    if (!out_ok[i]) {
+                        *first_bad = i;
+                        break;
+                    }
+        } else if (mode == 0) {
+            std::memcpy(out_dig, ctx.zc.h_dig, n * 8);
+        }
+        return PCS_OK;
+    }
     const uint8_t* base = static_cast<const uint8_t*>(pages[0]);
     const bool direct = contiguous_pinned(pages, n, P);
     for (auto& s : ctx.slot)
@@ -287,6 +423,7 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
         if ((rc = drain(s))) break;
         const uint64_t cnt = std::min(chunk, n - first);
         if (!direct) gather(s.h_pages, pages, first, cnt, P);
+        count(direct ? PCS_COUNTER_DIRECT_DMA_CHUNKS : PCS_COUNTER_GATHER_CHUNKS);
         s.first = first;
         s.count = cnt;
         e = hipMemcpyAsync(s.d_pages, direct ? base + first * P : s.h_pages, cnt * P, hipMemcpyHostToDevice,
@@ -358,6 +495,8 @@ struct pcs_batch {
     uint8_t* d_ok = nullptr;
     size_t cap_bytes = 0, cap_n = 0;
     std::vector<void*> stamp_pages;
+    ZcBufs zc;
+    bool zero_copy = false;  // in-flight batch reads registered pages in place
     uint64_t n = 0, P = 0, first_bad = UINT64_MAX;
     int mode = 0, state = 0;  // 0 idle, 1 in flight, 2 done, -1 failed
 };
@@ -365,7 +504,17 @@ struct pcs_batch {
 namespace {
 int batch_finalize(pcs_batch* b) {
     b->first_bad = UINT64_MAX;
-    if (b->mode == PCS_BATCH_VALIDATE) {
+    if (b->zero_copy) {  // results already in host memory, pages stamped in place
+        if (b->n) std::memcpy(b->mode == PCS_BATCH_VALIDATE ? static_cast<void*>(b->h_ok) : b->h_dig,
+                              b->mode == PCS_BATCH_VALIDATE ? static_cast<void*>(b->zc.h_ok) : b->zc.h_dig,
+                              b->mode == PCS_BATCH_VALIDATE ? b->n : b->n * 8);
+        if (b->mode == PCS_BATCH_VALIDATE)
+            for (uint64_t i = 0; i < b->n; ++i)
+                if (!b->h_ok[i]) {
+                    b->first_bad = i;
+                    break;
+                }
+    } else if (b->mode == PCS_BATCH_VALIDATE) {
         for (uint64_t i = 0; i < b->n; ++i)
             if (!b->h_ok[i]) {
                 b->first_bad = i;
@@ -466,12 +615,56 @@ int pcs_host_alloc_pinned(uint64_t bytes, void** out) {
         *out = nullptr;
         return fail(PCS_ERR_NOMEM, "hipHostMalloc failed");
     }
+    if (int rc = add_region(*out, bytes ? bytes : 1, true)) {
+        (void)hipHostFree(*out);
+        *out = nullptr;
+        return rc;
+    }
     return PCS_OK;
 }
 
 int pcs_host_free_pinned(void* p) {
     if (!p) return PCS_OK;
+    {
+        std::unique_lock lk(g_reg_mu);
+        auto it = g_regions.find(reinterpret_cast<uintptr_t>(p));
+        if (it == g_regions.end() || !it->second.allocated)
+            return fail(PCS_ERR_INVALID, "not a pcs_host_alloc_pinned allocation");
+        g_regions.erase(it);
+    }
     return finish(hipHostFree(p), "hipHostFree");
+}
+
+int pcs_host_register(void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return fail(PCS_ERR_INVALID, "null pointer or zero size");
+    if (int rc = require_device()) return rc;
+    {
+        std::shared_lock lk(g_reg_mu);  // reject overlaps before pinning anything
+        const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+        auto it = g_regions.upper_bound(b);
+        if ((it != g_regions.end() && it->first < b + bytes) ||
+            (it != g_regions.begin() && std::prev(it)->first + std::prev(it)->second.bytes > b))
+            return fail(PCS_ERR_INVALID, "region overlaps a registered one");
+    }
+    hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+    if (int rc = add_region(p, bytes, false)) {
+        (void)hipHostUnregister(p);
+        return rc;
+    }
+    return PCS_OK;
+}
+
+int pcs_host_unregister(void* p) {
+    if (!p) return fail(PCS_ERR_INVALID, "null pointer");
+    {
+        std::unique_lock lk(g_reg_mu);
+        auto it = g_regions.find(reinterpret_cast<uintptr_t>(p));
+        if (it == g_regions.end() || it->second.allocated)
+            return fail(PCS_ERR_INVALID, "not the base of a pcs_host_register region");
+        g_regions.erase(it);
+    }
+    return finish(hipHostUnregister(p), "hipHostUnregister");
 }
 
 int pcs_batch_create(pcs_batch** out) {
@@ -538,9 +731,25 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
         b->first_bad = UINT64_MAX;
         return PCS_OK;
     }
+    hipStream_t s = b->stream;
+    b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
+    if (b->zero_copy) {
+        // stamp writes digests into the pages and into zc.h_dig (the digest
+        // result of a stamp batch)
+        e = pcs::run_list(mode, algo, b->zc.d_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
+                          mode == PCS_BATCH_VALIDATE ? b->zc.d_ok : nullptr, s);
+        if (e == hipSuccess) e = hipEventRecord(b->done, s);
+        if (e != hipSuccess) {
+            b->state = -1;
+            return hip_fail(e, "pcs_batch_submit (zero-copy)");
+        }
+        count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
+        b->state = 1;
+        return PCS_OK;
+    }
     const bool direct = contiguous_pinned(pages, n, P);
     if (!direct) gather(b->h_pages, pages, 0, n, P);
-    hipStream_t s = b->stream;
+    count(direct ? PCS_COUNTER_DIRECT_DMA_CHUNKS : PCS_COUNTER_GATHER_CHUNKS);
     e = hipMemcpyAsync(b->d_pages, direct ? pages[0] : b->h_pages, n * P, hipMemcpyHostToDevice, s);
     const int kmode = mode == PCS_BATCH_VALIDATE ? 1 : 0;
     if (e == hipSuccess) e = pcs::run_pages(kmode, algo, b->d_pages, P, n, b->d_dig, b->d_ok, nullptr, s);
@@ -615,6 +824,7 @@ int pcs_batch_destroy(pcs_batch* b) {
     (void)hipFree(b->d_dig);
     (void)hipHostFree(b->h_ok);
     (void)hipFree(b->d_ok);
+    b->zc.release();
     if (b->done) (void)hipEventDestroy(b->done);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -663,6 +873,10 @@ int pcs_set_tuning(int key, int64_t value) {
 }
 
 int64_t pcs_get_tuning(int key) { return pcs::get_tuning(key); }
+
+uint64_t pcs_counter(int which) {
+    return (which < 0 || which > 2) ? 0 : g_counters[which].load(std::memory_order_relaxed);
+}
 
 int pcs_gen_pages_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t seed, uint64_t first_page_index,
                       pcs_stream_t stream) {

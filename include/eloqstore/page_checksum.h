@@ -52,6 +52,13 @@ void SetChecksums(std::span<char* const> pages, size_t page_size, PageHash hash 
 void PageDigests(std::span<const char* const> pages, size_t page_size, uint64_t* digests_out,
                  PageHash hash = PageHash::XXH3_64);
 
+// Registers a page-pool chunk or io_uring buffer ring once (PagesPool::Extend,
+// src/storage/page.cpp:95-120): batches whose pages all lie in registered
+// memory are then hashed in place over PCIe in one launch, with no gather
+// copy (pcs_host_register).  Unregister only when no batch over it is in flight.
+void RegisterPagePool(void* base, size_t bytes);
+void UnregisterPagePool(void* base);
+
 // Asynchronous batch for coroutine call sites: Submit, then Poll() from the
 // shard work loop (shard.cpp:67-130) until it returns true.  Pages must stay
 // valid until then; SubmitStamp writes the digests into them on completion.

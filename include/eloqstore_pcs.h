@@ -122,9 +122,25 @@ int pcs_pages_digest_host(const void *const *pages, uint64_t page_size, uint64_t
                           int algo, uint64_t *digests);
 
 /* Pinned (page-locked) host memory, e.g. for an io_uring buffer ring or file
- * staging: batches over one contiguous pinned run are DMA'd with no gather. */
+ * staging: batches over one contiguous pinned run are DMA'd with no gather.
+ * The allocation is also a registered region (below). */
 int pcs_host_alloc_pinned(uint64_t bytes, void **out);
 int pcs_host_free_pinned(void *p);
+
+/* Registered page pools (zero-copy).  EloqStore allocates its page pool in
+ * chunks of 1024 pages (PagesPool::Extend, src/storage/page.cpp:95-120) and
+ * its io_uring buffer rings once at start-up.  Registering such a region once
+ * (page-locks it and maps it for the GPU) lets a host batch read and write its
+ * pages in place over PCIe.  A host batch (pcs_pages_*_host, pcs_batch_submit)
+ * whose pages all lie in registered regions, are 16-byte aligned and have a
+ * fast size (XXH3: page_size % 256 == 0; XXH64: page_size % 64 == 0 and
+ * >= 128) runs as ONE kernel launch.  That launch reads the page list and the
+ * pages from host memory and writes the verdicts, digests or stamped headers
+ * straight back: no gather copy and no staging DMA
+ * (PCS_TUNE_ZERO_COPY).  Regions must not overlap.  A region must stay
+ * registered until every batch over it has completed. */
+int pcs_host_register(void *ptr, uint64_t bytes);
+int pcs_host_unregister(void *ptr);  /* ptr = the base passed to pcs_host_register */
 
 /* ---- asynchronous host batches (shard-loop integration) --------------------
  * EloqStore's shard thread never blocks: its work loop is Submit() ->
@@ -180,7 +196,7 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_XXH64_NT_LOADS       [0] same for the XXH64 page kernels (their
  *                                     64-byte-per-page pieces lose the line's
  *                                     other half under nt: measured slower)
- *   PCS_TUNE_STAMP_BYTES        [128] bytes of each page a fixed-size XXH3
+ *   PCS_TUNE_STAMP_BYTES          [0] bytes of each page a fixed-size XXH3
  *                                     stamp rewrites (8, 64, 128 or 256): the
  *                                     digest plus the unchanged bytes after it;
  *                                     0 = two passes (digest kernel into a
@@ -188,7 +204,11 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_XXH64_LAYOUT         [0] 0 = 16-lane 256 B loads with an LDS hand-
  *                                     off to the hashing quads (uses
  *                                     PCS_TUNE_NT_LOADS); 1 = each quad loads
- *                                     its own 64 B pieces */
+ *                                     its own 64 B pieces
+ *   PCS_TUNE_ZERO_COPY            [1] host batches over registered pages:
+ *                                     1 = zero-copy (one launch, pages read in
+ *                                     place); 0 = stage through device memory
+ *                                     (gather or direct DMA) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -196,9 +216,19 @@ enum pcs_tune_key {
     PCS_TUNE_XXH64_NT_LOADS = 4,
     PCS_TUNE_STAMP_BYTES = 5,
     PCS_TUNE_XXH64_LAYOUT = 6,
+    PCS_TUNE_ZERO_COPY = 7,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
+
+/* ---- path counters ----------------------------------------------------------
+ * Process-wide counts of how host batches were served (monotonic). */
+enum pcs_counter {
+    PCS_COUNTER_ZERO_COPY_LAUNCHES = 0, /* registered pages hashed in place */
+    PCS_COUNTER_DIRECT_DMA_CHUNKS = 1,  /* contiguous pinned runs DMA'd as is */
+    PCS_COUNTER_GATHER_CHUNKS = 2,      /* pages gathered into pinned staging */
+};
+uint64_t pcs_counter(int which); /* 0 for an unknown counter */
 
 /* ---- workload tooling (benchmarks, tests, scrub drills) -------------------
  * Synthetic pages: word w of page p = splitmix64((seed ^ p) + (w+1) *

@@ -34,7 +34,8 @@ def test_cpp_dropin_symbols_exported():
     for sym in ("eloqstore::SetChecksum(std::basic_string_view<char, std::char_traits<char> >)",
                 "eloqstore::ValidateChecksum(std::basic_string_view<char, std::char_traits<char> >)",
                 "eloqstore::ValidateChecksums(", "eloqstore::SetChecksums(", "eloqstore::PageDigests(",
-                "eloqstore::ChecksumBatch::Poll()", "eloqstore::ManifestChecksum(", "eloqstore::ValidateManifestRecord("):
+                "eloqstore::ChecksumBatch::Poll()", "eloqstore::ManifestChecksum(", "eloqstore::ValidateManifestRecord(",
+                "eloqstore::RegisterPagePool(", "eloqstore::UnregisterPagePool("):
         assert sym in out, sym
 
 
@@ -52,7 +53,8 @@ def test_no_gpu_fails_loudly():
                      ("pcs_pages_stamp_dev", (0, 4096, 1, 0, 0)),
                      ("pcs_desc_digest_dev", (0, 0, 0, 1, 0, 0, 0)),
                      ("pcs_xxh3_64_ranges_dev", (0, 0, 0, 1, 0, 0)),
-                     ("pcs_gen_pages_dev", (0, 4096, 1, 0, 0, 0))):
+                     ("pcs_gen_pages_dev", (0, 4096, 1, 0, 0, 0)),
+                     ("pcs_host_register", (4096, 4096))):
         assert getattr(so, fn)(*args) == pcs.PCS_ERR_NO_DEVICE, fn
     with pytest.raises(pcs.PcsError):
         pcs.validate_checksum(bytearray(4096))
@@ -107,3 +109,10 @@ def test_cli_without_gpu_fails_loudly(tmp_path):
     r = run_tool(str(f), "010")  # octal 8, as std::stoull(base 0) parses it
     assert r.returncode not in (0, 2)
     assert "no usable HIP device" in r.stderr
+
+
+def test_counters_and_tuning_defaults():
+    assert pcs.counter(pcs.COUNTER_ZERO_COPY_LAUNCHES) >= 0
+    assert pcs.lib().pcs_counter(99) == 0
+    assert pcs.get_tuning(pcs.TUNE_ZERO_COPY) == 1
+    assert pcs.get_tuning(pcs.TUNE_STAMP_BYTES) == 0

@@ -1,0 +1,142 @@
+"""Zero-copy host batches over registered page pools (pcs_host_register).
+
+EloqStore's pages live in pool chunks of 1024 pages (PagesPool::Extend,
+src/storage/page.cpp:95-120) and are handed to the checksum call sites as
+scattered pointers (ReadPages, async_io_manager.cpp:353-366; FlushBatchPages,
+write_task.cpp:155-167).  With the chunk registered, a batch is one kernel
+launch that reads the pages in place over PCIe.  Every result is checked
+against the CPU oracle; the path counters prove which path ran.
+"""
+import numpy as np
+import pytest
+
+import eloqstore_amd as pcs
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ZC = pcs.COUNTER_ZERO_COPY_LAUNCHES
+GATHER = pcs.COUNTER_GATHER_CHUNKS
+
+
+def _zc_delta(fn):
+    before = (pcs.counter(ZC), pcs.counter(GATHER))
+    out = fn()
+    return out, pcs.counter(ZC) - before[0], pcs.counter(GATHER) - before[1]
+
+
+def _scattered(pool, n, seed):
+    """A ReadPages-like pointer list: distinct pool pages in random order."""
+    idx = np.random.default_rng(seed).permutation(pool.n)[:n]
+    return idx, pool.ptr(idx)
+
+
+@pytest.mark.parametrize("algo,P", [(0, 4096), (0, 16384), (0, 65536), (0, 1280), (1, 4096), (1, 8192), (1, 192)])
+def test_zero_copy_digest_validate_stamp(algo, P):
+    n_pool = 1024 if P <= 16384 else 64  # one PagesPool chunk (page.cpp:95-120)
+    with pcs.PagePool(n_pool, P) as pool:
+        pool.pages[:] = oracle.fill_pages(P, n_pool, 0x2C0 + P).reshape(n_pool, P)
+        want = oracle.pages_digest(pool.pages, P, algo)
+        idx, ptrs = _scattered(pool, min(300, n_pool), seed=P)
+
+        dig, zc, g = _zc_delta(lambda: pcs.digest_ptrs(ptrs, P, algo))
+        assert zc == 1 and g == 0
+        assert np.array_equal(dig, want[idx])
+
+        _, zc, _ = _zc_delta(lambda: pcs.stamp_ptrs(ptrs, P, algo))
+        assert zc == 1
+        stamped = pool.pages[idx, :8].copy().view(np.uint64).ravel()
+        assert np.array_equal(stamped, want[idx])
+
+        (ok, fb), zc, _ = _zc_delta(lambda: pcs.validate_ptrs(ptrs, P, algo))
+        assert zc == 1 and ok.all() and fb is None
+
+        # persist.cpp:241-246 style corruption: byte 10 of every 7th listed page
+        bad = idx[::7]
+        pool.pages[bad, 10] ^= 0xFF
+        ok, fb = pcs.validate_ptrs(ptrs, P, algo)
+        assert np.array_equal(np.flatnonzero(ok == 0), np.arange(0, len(idx), 7))
+        assert fb == 0
+
+
+def test_zero_copy_sees_host_rewrites():
+    """The pool is reused batch after batch: the GPU must never serve a page
+    from a stale cached copy after the host rewrote it."""
+    P = 4096
+    with pcs.PagePool(256, P) as pool:
+        ptrs = pool.ptr(np.arange(256))
+        for round_ in range(4):
+            pool.pages[:] = oracle.fill_pages(P, 256, 0x900 + round_).reshape(256, P)
+            want = oracle.pages_digest(pool.pages, P, 0)
+            assert np.array_equal(pcs.digest_ptrs(ptrs, P), want)
+            pcs.stamp_ptrs(ptrs, P)
+            assert np.array_equal(pool.pages[:, :8].copy().view(np.uint64).ravel(), want)
+            ok, fb = pcs.validate_ptrs(ptrs, P)
+            assert ok.all() and fb is None
+
+
+def test_zero_copy_async_batch():
+    P = 4096
+    with pcs.PagePool(512, P) as pool:
+        pool.pages[:] = oracle.fill_pages(P, 512, 0x77).reshape(512, P)
+        want = oracle.pages_digest(pool.pages, P, 0)
+        idx, ptrs = _scattered(pool, 128, seed=5)  # max_read_pages_batch (kv_options.h:18-19)
+        b = pcs.Batch()
+        try:
+            before = pcs.counter(ZC)
+            b.submit_ptrs(pcs.Batch.STAMP, ptrs, P)
+            b.wait()
+            assert pcs.counter(ZC) == before + 1
+            assert b.result() == [int(x) for x in want[idx]]
+            assert np.array_equal(pool.pages[idx, :8].copy().view(np.uint64).ravel(), want[idx])
+            pool.pages[idx[3], 100] ^= 1
+            b.submit_ptrs(pcs.Batch.VALIDATE, ptrs, P)
+            while not b.poll():
+                pass
+            ok, fb = b.result()
+            assert fb == 3 and ok.count(0) == 1
+        finally:
+            b.close()
+
+
+def test_partially_registered_batch_falls_back():
+    """One page outside every registered region: the staging path runs, same results."""
+    P = 4096
+    with pcs.PagePool(64, P) as pool, pcs.PagePool(8, P, register=False) as loose:
+        pool.pages[:] = oracle.fill_pages(P, 64, 1).reshape(64, P)
+        loose.pages[:] = oracle.fill_pages(P, 8, 2).reshape(8, P)
+        ptrs = np.concatenate([pool.ptr(np.arange(10)), loose.ptr([3])])
+        want = np.concatenate([oracle.pages_digest(pool.pages[:10], P), oracle.pages_digest(loose.pages[3:4], P)])
+        dig, zc, g = _zc_delta(lambda: pcs.digest_ptrs(ptrs, P))
+        assert zc == 0 and g == 1
+        assert np.array_equal(dig, want)
+
+
+def test_zero_copy_policy_knob():
+    P = 4096
+    with pcs.PagePool(64, P) as pool:
+        pool.pages[:] = oracle.fill_pages(P, 64, 3).reshape(64, P)
+        want = oracle.pages_digest(pool.pages, P)
+        contiguous = pool.ptr(np.arange(64))
+        old = pcs.get_tuning(pcs.TUNE_ZERO_COPY)
+        try:
+            pcs.set_tuning(pcs.TUNE_ZERO_COPY, 0)  # stage: gather, or direct DMA of a contiguous run
+            dig, zc, g = _zc_delta(lambda: pcs.digest_ptrs(contiguous[::-1], P))
+            assert zc == 0 and g == 1 and np.array_equal(dig, want[::-1])
+            before = pcs.counter(pcs.COUNTER_DIRECT_DMA_CHUNKS)
+            dig, zc, _ = _zc_delta(lambda: pcs.digest_ptrs(contiguous, P))
+            assert zc == 0 and pcs.counter(pcs.COUNTER_DIRECT_DMA_CHUNKS) == before + 1
+            assert np.array_equal(dig, want)
+            pcs.set_tuning(pcs.TUNE_ZERO_COPY, 1)  # registered -> zero-copy, contiguous or not
+            dig, zc, _ = _zc_delta(lambda: pcs.digest_ptrs(contiguous, P))
+            assert zc == 1 and np.array_equal(dig, want)
+        finally:
+            pcs.set_tuning(pcs.TUNE_ZERO_COPY, old)
+
+
+def test_register_rejects_overlap_and_bad_unregister():
+    with pcs.PagePool(16, 4096) as pool:
+        with pytest.raises(pcs.PcsError):
+            pcs.host_register(pool.base + 4096, 4096)
+        with pytest.raises(pcs.PcsError):
+            pcs.host_unregister(pool.base + 4096)
