@@ -247,8 +247,49 @@ struct Variant {
     std::vector<float> ms;
 };
 
+// G: 64 KiB pages, one workgroup per page: group j reads the page's 4 KiB
+// slice j (the shape of a split long-page hash: block sums in parallel, one
+// short serial chain per page).
+template <bool NT>
+__global__ __launch_bounds__(256) void k_wg_page64k(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    const int g = threadIdx.x & 15, j = threadIdx.x >> 4;
+    for (uint64_t pg = blockIdx.x; pg < n; pg += gridDim.x) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * 65536 + j * 4096) + g;
+        u32x4 d[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) d[c] = ld<NT>(base + c * 16);
+        uint32_t r = 0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) r += fold(d[c]);
+        if (r == 0x12345678u) out[pg] = r;
+    }
+}
+
+// A5: product-like 64 KiB: 16-lane group per page, 4 KiB batches in sequence.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_group16_big(const uint8_t* __restrict__ pages, uint64_t n, uint64_t* out) {
+    const int g = threadIdx.x & 15;
+    const uint64_t ngroups = (uint64_t)gridDim.x * 16;
+    for (uint64_t pg = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4; pg < n; pg += ngroups) {
+        uint32_t r = 0;
+        for (int b = 0; b < 16; ++b) {
+            const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * 65536 + b * 4096) + g;
+            u32x4 d[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) d[c] = ld<NT>(base + c * 16);
+#pragma unroll
+            for (int c = 0; c < 16; ++c) r += fold(d[c]);
+        }
+        if (r == 0x12345678u) out[pg] = r;
+    }
+}
+
+struct Variant;
+static int main_big(int rounds);
+
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
+    if (argc > 2 && std::string(argv[2]) == "big") return main_big(rounds);
     const uint64_t P = 4096, n = 1 << 20, bytes = n * P;
     uint8_t* pages;
     uint64_t* out;
@@ -343,6 +384,63 @@ int main(int argc, char** argv) {
         const float med = v.ms[v.ms.size() / 2];
         std::printf("%-34s %9.4f %9.1f %9.1f\n", v.name.c_str(), med, bytes / (med * 1e-3) / 1e9,
                     bytes / (v.ms[0] * 1e-3) / 1e9);
+    }
+    return 0;
+}
+
+// 64 KiB pages x 256 K = 16 GiB (config 4): is the product's shortfall there
+// the access pattern or the buffer size?
+static int main_big(int rounds) {
+    const uint64_t P = 65536, n = 1 << 18, bytes = n * P;
+    uint8_t* pages;
+    uint64_t* out;
+    CK(hipMalloc(&pages, bytes));
+    CK(hipMalloc(&out, n * 16 * 8));
+    if (pcs_gen_pages_dev(pages, P, n, 0x5EED0004, 0, nullptr)) std::exit(2);
+    CK(hipDeviceSynchronize());
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    struct V { std::string name; std::function<void(hipStream_t)> run; uint64_t bytes; std::vector<float> ms; };
+    std::vector<V> vs;
+    auto add = [&](std::string name, uint64_t b, std::function<void(hipStream_t)> f) { vs.push_back({name, f, b, {}}); };
+    add("4K-page group16 nt over 16 GiB", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_group16<4096, true>), dim3(n * 16 / 16), dim3(256), 0, st, pages, n * 16, out); });
+    add("4K-page group16 nt over 4 GiB", bytes / 4, [=](hipStream_t st) { hipLaunchKernelGGL((k_group16<4096, true>), dim3(n * 4 / 16), dim3(256), 0, st, pages, n * 4, out); });
+    add("4K-page xcd tiles over 16 GiB", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_xcd<4096>), dim3(n), dim3(256), 0, st, pages, n * 16, out); });
+    for (int bpc : {8, 16})
+        add("linear U8 nt bpc=" + std::to_string(bpc), bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_linear<8, true>), dim3(cus * bpc), dim3(256), 0, st, pages, bytes / 16, out); });
+    for (int bpc : {4, 8, 16})
+        add("group16-big nt bpc=" + std::to_string(bpc), bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_big<true>), dim3(cus * bpc), dim3(256), 0, st, pages, n, out); });
+    add("group16-big nt nonpersistent", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_big<true>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
+    for (int bpc : {4, 8})
+        add("wg-per-page nt bpc=" + std::to_string(bpc), bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_wg_page64k<true>), dim3(cus * bpc), dim3(256), 0, st, pages, n, out); });
+    add("wg-per-page nt nonpersistent", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_wg_page64k<true>), dim3(n), dim3(256), 0, st, pages, n, out); });
+    add("wg-per-page plain nonpersistent", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_wg_page64k<false>), dim3(n), dim3(256), 0, st, pages, n, out); });
+    add("PRODUCT pcs_read_ceiling_dev 64K", bytes, [=](hipStream_t st) { pcs_read_ceiling_dev(pages, P, n, out, (pcs_stream_t)st); });
+    add("PRODUCT pcs_pages_digest_dev xxh3 64K", bytes, [=](hipStream_t st) { pcs_pages_digest_dev(pages, P, n, 0, out, (pcs_stream_t)st); });
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (auto& v : vs) v.run(s);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < rounds; ++r)
+        for (auto& v : vs) {
+            hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 200000LL);
+            CK(hipEventRecord(a, s));
+            v.run(s);
+            CK(hipEventRecord(b, s));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.ms.push_back(ms);
+        }
+    CK(hipGetLastError());
+    std::printf("%-40s %9s %9s %9s\n", "variant (64 KiB pages, 16 GiB)", "med_ms", "GB/s", "best GB/s");
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const float med = v.ms[v.ms.size() / 2];
+        std::printf("%-40s %9.4f %9.1f %9.1f\n", v.name.c_str(), med, v.bytes / (med * 1e-3) / 1e9, v.bytes / (v.ms[0] * 1e-3) / 1e9);
     }
     return 0;
 }
