@@ -146,6 +146,10 @@ TUNE_XXH64_NT_LOADS = 4
 TUNE_STAMP_BYTES = 5
 TUNE_XXH64_LAYOUT = 6
 TUNE_ZERO_COPY = 7
+TUNE_XXH3_RT_BATCH = 8
+TUNE_XXH3_SPLIT_PAGES = 9
+TUNE_DESC_SORT = 10
+TUNE_INLINE_LIST = 11
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -28,8 +28,10 @@ inline bool list_shape_ok(int algo, uint64_t P) {
     return algo == 0 ? (P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull)
                      : (P % 64 == 0 && P >= 128 && P <= 0xFFFFFFFFull);
 }
-hipError_t run_list(int mode, int algo, const uint64_t* ptrs, uint64_t page_size, uint64_t n, uint64_t* out,
-                    uint8_t* ok, hipStream_t s);
+// host_ptrs, if given, is a host-readable copy of the list: small batches
+// pass it in the kernel arguments instead.
+hipError_t run_list(int mode, int algo, const uint64_t* ptrs, const uint64_t* host_ptrs, uint64_t page_size,
+                    uint64_t n, uint64_t* out, uint8_t* ok, hipStream_t s);
 
 hipError_t run_gen_pages(uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t seed, uint64_t first_page,
                          hipStream_t s);

@@ -363,7 +363,7 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
         // verdicts / digests / page headers straight to host memory.
         if (int rc = ensure_slot(ctx.slot[0], 0, 1)) return rc;
         hipStream_t zs = ctx.slot[0].stream;
-        e = pcs::run_list(mode, algo, ctx.zc.d_ptrs, P, n, mode == 0 ? ctx.zc.d_dig : nullptr,
+        e = pcs::run_list(mode, algo, ctx.zc.d_ptrs, ctx.zc.h_ptrs, P, n, mode == 0 ? ctx.zc.d_dig : nullptr,
                           mode == 1 ? ctx.zc.d_ok : nullptr, zs);
         if (e == hipSuccess) e = hipStreamSynchronize(zs);
         if (e != hipSuccess) return hip_fail(e, "zero-copy page list");
@@ -736,7 +736,7 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
     if (b->zero_copy) {
         // stamp writes digests into the pages and into zc.h_dig (the digest
         // result of a stamp batch)
-        e = pcs::run_list(mode, algo, b->zc.d_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
+        e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
                           mode == PCS_BATCH_VALIDATE ? b->zc.d_ok : nullptr, s);
         if (e == hipSuccess) e = hipEventRecord(b->done, s);
         if (e != hipSuccess) {

@@ -25,6 +25,7 @@
 #include "eloqstore_pcs_internal.h"
 
 #include <algorithm>
+#include <cstring>
 #include <atomic>
 #include <mutex>
 
@@ -154,7 +155,9 @@ __device__ __forceinline__ Xxh3Lane make_xxh3_lane(int g) {
 // word, the last stripe (page words P/8-8 .. P/8-1, held by lanes 12..15 of
 // the final chunk) keyed with secret + 121, and page words P/8-7 .. P/8-1
 // excluded from the ordinary stripes (xxhash.h:6005-6016).
-template <bool FINAL>
+// NOCARRY leaves out the block's last input word (the carry, page word
+// 128(b+1)); the caller adds its two terms later (split-page kernel).
+template <bool FINAL, bool NOCARRY = false>
 __device__ __forceinline__ void xxh3_block_terms(const Xxh3Lane& L, const u32x4 (&d)[4], uint64_t carry,
                                                  int nchunks, uint64_t& Te, uint64_t& To) {
     uint64_t Ue = 0, Uo = 0, Ve = 0, Vo = 0;
@@ -166,7 +169,7 @@ __device__ __forceinline__ void xxh3_block_terms(const Xxh3Lane& L, const u32x4 
         const uint64_t w1 = hi64(d[c]);
         bool use0 = true, use1 = true;
         if (c == 0) {
-            if (FINAL) use0 = (g != 0);
+            if (FINAL || NOCARRY) use0 = (g != 0);
             else w0 = (g == 0) ? carry : w0;
         }
         if (FINAL && c == nchunks - 1 && g >= 12) {
@@ -280,6 +283,52 @@ __device__ __forceinline__ uint64_t xxh3_page_rt(const uint8_t* __restrict__ pag
     return xxh3_merge(L, Ae + Te, Ao + To, (uint64_t)(P - 8));
 }
 
+// Run-time page size with the fixed kernel's batching: up to 4 blocks (4 KiB
+// per group, 16 KiB per wave) are loaded before any is folded, so mixed-size
+// batches keep as many bytes in flight as the fixed-size kernel.  Groups of a
+// wave may have different page sizes; the loop then runs to the largest with
+// the others masked.
+template <bool NT>
+__device__ __forceinline__ uint64_t xxh3_page_rt4(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
+                                                  uint64_t& stored) {
+    const int NB = (int)((P - 9) / 1024);
+    const int R = (int)(P / 256) - 4 * NB;
+    const int TB = NB + 1;
+    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
+    uint64_t Ae = L.init_e, Ao = L.init_o;
+    u32x4 head = ld16<NT>(base);
+    stored = lo64(head);
+    for (int b0 = 0; b0 < TB; b0 += 4) {
+        u32x4 d[5][4];
+        d[0][0] = head;
+#pragma unroll
+        for (int i = 0; i <= 4; ++i) {
+            const int b = b0 + i;
+            const int nc = (b >= TB) ? 0 : (i == 4) ? 1 : (b == NB) ? R : 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < nc && !(i == 0 && c == 0)) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int b = b0 + i;
+            if (b < NB) {
+                uint64_t Te, To;
+                xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
+                Ae = xxh3_scramble(Ae + Te, L.ks_e);
+                Ao = xxh3_scramble(Ao + To, L.ks_o);
+            } else if (b == NB) {
+                uint64_t Te, To;
+                xxh3_block_terms<true>(L, d[i], 0, R, Te, To);
+                Ae += Te;
+                Ao += To;
+            }
+        }
+        head = d[4][0];
+    }
+    return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
+}
+
 __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
     return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
 }
@@ -357,8 +406,97 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
     }
 }
 
+// Split pages (P = 8, 16, 32 or 64 KiB): G = P / 4096 groups share a page,
+// group j loading its 4 KiB slice (blocks 4j .. 4j+3) at once, so a
+// workgroup streams 64 KiB of contiguous page bytes instead of 16 separate
+// pages.  XXH3's long loop is acc <- scramble(acc + S_b) over block sums S_b
+// that depend on the data only (xxhash.h:5988-6017), so the groups compute
+// their S_b in parallel into LDS and one group per page then runs the short
+// serial chain (the long-range kernel's scheme, k_xxh3_long).  A slice's last
+// block needs the next slice's first word (its carry); it is left out of the
+// group's sum and added by the chain from the word the next group publishes.
+template <int P, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ pages, uint64_t n,
+                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                   unsigned long long* first_bad) {
+    static_assert(P % 4096 == 0 && P >= 8192 && P <= 65536, "split pages are 8..64 KiB");
+    constexpr int G = P / 4096;        // groups per page
+    constexpr int PPB = 16 / G;        // pages per 256-thread block
+    constexpr int NB = P / 1024 - 1;   // full blocks (xxhash.h:5996); block NB is the final one, 4 chunks
+    __shared__ uint64_t S[PPB][NB + 1][4][2];  // block sums per accumulator pair (even, odd)
+    __shared__ uint64_t C[PPB][G];             // first input word of each slice (the previous block's carry)
+    __shared__ uint64_t tile_h[16];
+    __shared__ uint8_t tile_ok[16];
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const int grp = threadIdx.x >> 4, ps = grp / G, j = grp % G, p = L.g & 3;
+    const uint64_t ntiles = (n + PPB - 1) / PPB;
+    const bool remap = gridDim.x == ntiles;
+    const uint64_t k22 = c_keys.acc[22];  // key of a block's last input word (stripe 15, lane 7)
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
+        const uint64_t pg = t * PPB + ps;
+        uint64_t stored = 0;
+        if (pg < n) {
+            const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P + 4096u * j) + L.g;
+            u32x4 d[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) d[i][c] = ld16<NT>(base + i * 64 + c * 16);
+            stored = lo64(d[0][0]);
+            if (L.g == 0) C[ps][j] = lo64(d[0][0]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint64_t Te, To;
+                if (i < 3) xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
+                else if (j < G - 1) xxh3_block_terms<false, true>(L, d[i], 0, 4, Te, To);
+                else xxh3_block_terms<true>(L, d[i], 0, 4, Te, To);
+                if (L.g < 4) {
+                    S[ps][4 * j + i][p][0] = Te;
+                    S[ps][4 * j + i][p][1] = To;
+                }
+            }
+        }
+        __syncthreads();
+        if (j == 0 && pg < n) {
+            uint64_t Ae = L.init_e, Ao = L.init_o;
+#pragma unroll 4
+            for (int b = 0; b < NB; ++b) {
+                uint64_t Te = S[ps][b][p][0], To = S[ps][b][p][1];
+                if ((b & 3) == 3 && p == 3) {  // slice boundary: add the carry word's terms
+                    const uint64_t cw = C[ps][(b + 1) >> 2];
+                    Te += cw;
+                    To += mul32x32(cw ^ k22);
+                }
+                Ae = xxh3_scramble(Ae + Te, L.ks_e);
+                Ao = xxh3_scramble(Ao + To, L.ks_o);
+            }
+            const uint64_t h = xxh3_merge(L, Ae + S[ps][NB][p][0], Ao + S[ps][NB][p][1], (uint64_t)(P - 8));
+            if (L.g == 0) {
+                tile_h[ps] = h;
+                tile_ok[ps] = (h == stored) ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        const uint64_t i0 = t * PPB;
+        if (threadIdx.x < PPB && i0 + threadIdx.x < n) {
+            if (MODE == kDigest || out) st_nt(out + i0 + threadIdx.x, tile_h[threadIdx.x]);
+            if (MODE == kValidate) st_nt(ok + i0 + threadIdx.x, tile_ok[threadIdx.x]);
+        }
+        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+            for (int k = 0; k < PPB && i0 + k < n; ++k)
+                if (!tile_ok[k]) {
+                    note_bad(first_bad, i0 + k);
+                    break;
+                }
+        }
+        // the next tile's writes to S / tile_h wait for everyone's reads here
+        __syncthreads();
+    }
+}
+
 // Fixed stride, run-time page size.
-template <int MODE, bool NT>
+template <int MODE, bool NT, bool B4>
 __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                     uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                     unsigned long long* first_bad) {
@@ -370,31 +508,55 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
         if (pg >= n) continue;
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
-        const uint64_t h = xxh3_page_rt<NT>(page, P, L, stored);
+        const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
 
 // Descriptor batch (mixed sizes).  Pages that miss the fast-path shape are
 // left to k_generic_desc.
-template <int MODE, bool NT>
+template <int MODE, bool NT, bool B4, bool SORT>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                   unsigned long long* first_bad) {
+    // SORT: the 16 pages of a tile are handed to the groups in order of size,
+    // so the four groups of a wave mostly share one size and none idles while
+    // a neighbour walks a longer page (mixed-size batches, config 3).
+    __shared__ uint8_t perm[16];
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 16 + (threadIdx.x >> 4);
-        if (pg >= n) continue;
-        const uint64_t o = off[pg];
-        const uint32_t P = len[pg];
-        if (!xxh3_fast_ok(o, P)) continue;
-        const uint8_t* page = base + o;
-        uint64_t stored = 0;
-        const uint64_t h = xxh3_page_rt<NT>(page, P, L, stored);
-        if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
+        int slot = threadIdx.x >> 4;
+        if constexpr (SORT) {
+            if (threadIdx.x < 16) {
+                const uint64_t i = t * 16 + threadIdx.x;
+                const uint32_t mine = i < n ? len[i] : 0xFFFFFFFFu;
+                int rank = 0;
+                for (int k = 0; k < 16; ++k) {
+                    const uint64_t ik = t * 16 + k;
+                    const uint32_t other = ik < n ? len[ik] : 0xFFFFFFFFu;
+                    rank += (other < mine) || (other == mine && k < (int)threadIdx.x);
+                }
+                perm[rank] = (uint8_t)threadIdx.x;
+            }
+            __syncthreads();
+            slot = perm[threadIdx.x >> 4];
+        }
+        const uint64_t pg = t * 16 + slot;
+        if (pg < n) {
+            const uint64_t o = off[pg];
+            const uint32_t P = len[pg];
+            if (xxh3_fast_ok(o, P)) {
+                const uint8_t* page = base + o;
+                uint64_t stored = 0;
+                const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
+                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+            }
+        }
+        if constexpr (SORT) __syncthreads();  // perm is rewritten by the next tile
     }
 }
 
@@ -404,24 +566,46 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
 // and the results live in pinned host memory too, so a batch is one launch.
 // PF > 0 uses the compile-time page size (a 4 KiB page is then one batch of
 // loads: one PCIe round trip instead of one per 1 KiB block).
-template <int MODE, int PF>
-__global__ __launch_bounds__(256) void k_xxh3_list(const uint64_t* __restrict__ ptrs, uint32_t P, uint64_t n,
-                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok) {
+template <int MODE, int PF, typename PageAt>
+__device__ __forceinline__ void xxh3_list_body(PageAt page_at, uint32_t P, uint64_t n, uint64_t* __restrict__ out,
+                                               uint8_t* __restrict__ ok) {
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     for (uint64_t t = blockIdx.x; t < (n + 15) / 16; t += gridDim.x) {
         const uint64_t pg = t * 16 + (threadIdx.x >> 4);
         if (pg >= n) continue;
-        const uint8_t* page = reinterpret_cast<const uint8_t*>(ptrs[pg]);
+        const uint8_t* page = page_at(pg);
         uint64_t stored = 0;
         uint64_t h;
         if constexpr (PF > 0) {
             u32x4 first;
             h = xxh3_page_fixed<PF, false>(page, L, stored, first);
         } else {
-            h = xxh3_page_rt<false>(page, P, L, stored);
+            h = xxh3_page_rt4<false>(page, P, L, stored);
         }
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, nullptr);
     }
+}
+
+template <int MODE, int PF>
+__global__ __launch_bounds__(256) void k_xxh3_list(const uint64_t* __restrict__ ptrs, uint32_t P, uint64_t n,
+                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    xxh3_list_body<MODE, PF>([=](uint64_t pg) { return reinterpret_cast<const uint8_t*>(ptrs[pg]); }, P, n, out, ok);
+}
+
+// Small batches (a ReadPages / FlushBatchPages batch is <= 256 pages,
+// kv_options.h:18-19, 70) carry the page list in the kernel arguments: the
+// waves then go straight to the pages instead of first fetching the list
+// from host memory, one PCIe round trip less.
+constexpr int kInlinePages = 256;
+struct InlineList {
+    uint64_t p[kInlinePages];
+};
+
+template <int MODE, int PF>
+__global__ __launch_bounds__(256) void k_xxh3_list_inl(InlineList list, uint32_t P, uint64_t n,
+                                                      uint64_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    xxh3_list_body<MODE, PF>([&](uint64_t pg) { return reinterpret_cast<const uint8_t*>(list.p[pg]); }, P, n, out,
+                             ok);
 }
 
 // ---------------------------------------------------------------------------
@@ -1083,23 +1267,28 @@ __global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pag
 }
 
 // Same loads, tile order and staged result stores as k_xxh3_fixed<P, kDigest>
-// with the hash replaced by an xor/add fold: the achievable rate of this
-// layout (the roofline's "measured ceiling").
-template <int P, bool NT>
+// (or, SPLIT, as k_xxh3_split<P, kDigest>: G = P / 4096 groups per page, one
+// 4 KiB slice each) with the hash replaced by an xor/add fold: the achievable
+// rate of the product's layout (the roofline's "measured ceiling").
+template <int P, bool NT, bool SPLIT>
 __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
                                                      uint64_t* __restrict__ out) {
+    constexpr int G = SPLIT ? P / 4096 : 1;  // groups per page
+    constexpr int PPB = 16 / G;              // pages per tile
+    constexpr int SLICE = P / G;             // bytes per group
     __shared__ uint64_t tile_r[16];
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const uint64_t ntiles = (n + 15) / 16;
+    const uint64_t ntiles = (n + PPB - 1) / PPB;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
         const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        const uint64_t pg = t * 16 + grp;
+        const uint64_t pg = t * PPB + grp / G;
         if (pg < n) {
-            const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P) + g;
+            const u32x4* base =
+                reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P + (uint64_t)SLICE * (grp % G)) + g;
             uint32_t x = 0, y = 0, z = 0, w = 0;
 #pragma unroll
-            for (int c = 0; c < P / 256; ++c) {
+            for (int c = 0; c < SLICE / 256; ++c) {
                 const u32x4 v = ld16<NT>(base + c * 16);
                 x ^= v.x; y += v.y; z ^= v.z; w += v.w;
             }
@@ -1111,8 +1300,13 @@ __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict_
             if (g == 0) tile_r[grp] = r;
         }
         __syncthreads();
-        const uint64_t i = t * 16 + threadIdx.x;
-        if (threadIdx.x < 16 && i < n) st_nt(out + i, tile_r[threadIdx.x]);
+        const uint64_t i = t * PPB + threadIdx.x;
+        if (threadIdx.x < PPB && i < n) {
+            uint64_t r = 0;
+#pragma unroll
+            for (int k = 0; k < G; ++k) r ^= tile_r[threadIdx.x * G + k];
+            st_nt(out + i, r);
+        }
         __syncthreads();
     }
 }
@@ -1156,15 +1350,22 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-std::atomic<int64_t> g_tune[8] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1, /*xxh64 nt*/ 0,
-                                  /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0, /*zero copy*/ 1};
+constexpr int kTuneKeys = 12;
+std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
+                                          /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
+                                          /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
+                                          /*xxh3 split pages from this size (0 = never)*/ 8192,
+                                          /*descriptor tiles sorted by page size*/ 0,
+                                          /*zero-copy page list in kernel arguments*/ 1};
 }
 int set_tuning(int key, int64_t value) {
-    if (key <= 0 || key >= 8 || value < 0) return -1;
+    if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
     g_tune[key].store(value, std::memory_order_relaxed);
     return 0;
 }
-int64_t get_tuning(int key) { return (key <= 0 || key >= 8) ? -1 : g_tune[key].load(std::memory_order_relaxed); }
+int64_t get_tuning(int key) {
+    return (key <= 0 || key >= kTuneKeys) ? -1 : g_tune[key].load(std::memory_order_relaxed);
+}
 
 namespace {
 // Page kernels: the knob caps the grid at that many 256-thread blocks per CU
@@ -1179,6 +1380,12 @@ unsigned page_grid(uint64_t n, unsigned pages_per_block, int key, uint64_t page_
     return (unsigned)(need < cap ? (need ? need : 1) : cap);
 }
 bool use_nt() { return g_tune[3].load(std::memory_order_relaxed) != 0; }
+// Fixed-size XXH3 pages hashed by k_xxh3_split (PCS_TUNE_XXH3_SPLIT_PAGES).
+bool split_pages(uint64_t P) {
+    const int64_t split = g_tune[9].load(std::memory_order_relaxed);
+    return split > 0 && P >= (uint64_t)split && P >= 8192 && P <= 65536 && (P & (P - 1)) == 0;
+}
+bool rt_batch4() { return g_tune[8].load(std::memory_order_relaxed) != 0; }
 bool use_nt64() { return g_tune[4].load(std::memory_order_relaxed) != 0; }
 bool xxh64_lds_layout() { return g_tune[6].load(std::memory_order_relaxed) != 1; }
 
@@ -1201,6 +1408,18 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
                              unsigned long long* fb, hipStream_t s) {
     const unsigned grid = page_grid(n, kBlock / 16, 1, P);  // kBlock/16 = one 16-page tile per block
     const int sb = (int)std::min<int64_t>(g_tune[5].load(std::memory_order_relaxed), 256);
+    if (MODE != kStamp && split_pages(P)) {
+        const uint64_t ppb = 16 / (P / 4096);
+        const uint64_t need = (n + ppb - 1) / ppb;
+        const unsigned g = (unsigned)std::min<uint64_t>(need, 0x7FFFFFFFull);
+        switch (P) {
+#define CASE(SZ) \
+    case SZ: hipLaunchKernelGGL((k_xxh3_split<SZ, MODE, NT>), dim3(g), dim3(kBlock), 0, s, pages, n, out, ok, fb); break;
+            CASE(8192) CASE(16384) CASE(32768) CASE(65536)
+#undef CASE
+        }
+        return hipGetLastError();
+    }
     switch (P) {
 #define CASE(SZ)                                                                                             \
     case SZ:                                                                                                 \
@@ -1209,8 +1428,12 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
         default:
-            hipLaunchKernelGGL((k_xxh3_stride<MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out,
-                               ok, fb);
+            if (rt_batch4())
+                hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, true>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
+                                   n, out, ok, fb);
+            else
+                hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, false>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
+                                   n, out, ok, fb);
     }
     return hipGetLastError();
 }
@@ -1285,10 +1508,21 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
         // fast kernels for conforming pages, generic lanes for the rest
         if (algo == 0) {
             const unsigned grid = page_grid(n, kBlock / 16, 1);
-            if (use_nt())
-                hipLaunchKernelGGL((k_xxh3_desc<MODE, true>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
-            else
-                hipLaunchKernelGGL((k_xxh3_desc<MODE, false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+#define L(NT_, B4_, SORT_) \
+    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_, SORT_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
+            const bool srt = g_tune[10].load(std::memory_order_relaxed) != 0;
+            if (use_nt()) {
+                if (rt_batch4()) {
+                    if (srt) L(true, true, true);
+                    else L(true, true, false);
+                } else {
+                    L(true, false, false);
+                }
+            } else {
+                if (rt_batch4()) L(false, true, false);
+                else L(false, false, false);
+            }
+#undef L
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
             if (xxh64_lds_layout()) {
@@ -1359,13 +1593,22 @@ hipError_t run_desc(int mode, int algo, const uint8_t* base, const uint64_t* off
     }
 }
 
-hipError_t run_list(int mode, int algo, const uint64_t* ptrs, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
-                    hipStream_t s) {
+hipError_t run_list(int mode, int algo, const uint64_t* ptrs, const uint64_t* host_ptrs, uint64_t P, uint64_t n,
+                    uint64_t* out, uint8_t* ok, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!list_shape_ok(algo, P)) return hipErrorNotSupported;
     if (algo == 0) {
         const unsigned grid = (unsigned)std::min<uint64_t>((n + 15) / 16, (uint64_t)cu_count() * kBlocksPerCu);
-#define LAUNCH(M, PF) hipLaunchKernelGGL((k_xxh3_list<M, PF>), dim3(grid), dim3(kBlock), 0, s, ptrs, (uint32_t)P, n, out, ok)
+        const bool inl = host_ptrs && n <= (uint64_t)kInlinePages && g_tune[11].load(std::memory_order_relaxed) != 0;
+        InlineList list;
+        if (inl) std::memcpy(list.p, host_ptrs, n * 8);
+#define LAUNCH(M, PF)                                                                                                \
+    do {                                                                                                             \
+        if (inl)                                                                                                     \
+            hipLaunchKernelGGL((k_xxh3_list_inl<M, PF>), dim3(grid), dim3(kBlock), 0, s, list, (uint32_t)P, n, out, ok); \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_xxh3_list<M, PF>), dim3(grid), dim3(kBlock), 0, s, ptrs, (uint32_t)P, n, out, ok);  \
+    } while (0)
 #define BY_SIZE(M)                                    \
     switch (P) {                                      \
         case 4096: LAUNCH(M, 4096); break;            \
@@ -1418,13 +1661,26 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 
 hipError_t run_read_ceiling(const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const unsigned grid = page_grid(n, kBlock / 16, 1);
     const bool nt = use_nt();
+    if (split_pages(P)) {  // mirror k_xxh3_split's tiles
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + 16 / (P / 4096) - 1) / (16 / (P / 4096)), 0x7FFFFFFFull);
+        switch (P) {
+#define CASE(SZ)                                                                                                  \
+    case SZ:                                                                                                      \
+        if (nt) hipLaunchKernelGGL((k_read_ceiling<SZ, true, true>), dim3(grid), dim3(kBlock), 0, s, pages, n, out);  \
+        else hipLaunchKernelGGL((k_read_ceiling<SZ, false, true>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); \
+        break;
+            CASE(8192) CASE(16384) CASE(32768) CASE(65536)
+#undef CASE
+        }
+        return hipGetLastError();
+    }
+    const unsigned grid = page_grid(n, kBlock / 16, 1);
     switch (P) {
-#define CASE(SZ)                                                                                            \
-    case SZ:                                                                                                \
-        if (nt) hipLaunchKernelGGL((k_read_ceiling<SZ, true>), dim3(grid), dim3(kBlock), 0, s, pages, n, out);  \
-        else hipLaunchKernelGGL((k_read_ceiling<SZ, false>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); \
+#define CASE(SZ)                                                                                                   \
+    case SZ:                                                                                                       \
+        if (nt) hipLaunchKernelGGL((k_read_ceiling<SZ, true, false>), dim3(grid), dim3(kBlock), 0, s, pages, n, out);  \
+        else hipLaunchKernelGGL((k_read_ceiling<SZ, false, false>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); \
         break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE

@@ -208,7 +208,23 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_ZERO_COPY            [1] host batches over registered pages:
  *                                     1 = zero-copy (one launch, pages read in
  *                                     place); 0 = stage through device memory
- *                                     (gather or direct DMA) */
+ *                                     (gather or direct DMA)
+ *   PCS_TUNE_XXH3_RT_BATCH        [1] XXH3 pages whose size is not a compiled
+ *                                     case (mixed-size descriptors, odd
+ *                                     multiples of 256): 1 = load 4 blocks per
+ *                                     step like the fixed kernels; 0 = one
+ *                                     block per step
+ *   PCS_TUNE_XXH3_SPLIT_PAGES  [8192] fixed-size XXH3 pages of at least this
+ *                                     many bytes (power of two, 8-64 KiB) are
+ *                                     split over P/4096 groups, one 4 KiB slice
+ *                                     each, with the scramble chain run from
+ *                                     block sums in LDS; 0 = never
+ *   PCS_TUNE_DESC_SORT            [0] XXH3 descriptor batches (nt loads, 4-block
+ *                                     batches): 1 = hand each tile's 16 pages
+ *                                     to the groups in order of size
+ *   PCS_TUNE_INLINE_LIST          [1] zero-copy XXH3 batches of <= 256 pages
+ *                                     pass the page list in the kernel
+ *                                     arguments (0 = read it from host memory) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -217,6 +233,10 @@ enum pcs_tune_key {
     PCS_TUNE_STAMP_BYTES = 5,
     PCS_TUNE_XXH64_LAYOUT = 6,
     PCS_TUNE_ZERO_COPY = 7,
+    PCS_TUNE_XXH3_RT_BATCH = 8,
+    PCS_TUNE_XXH3_SPLIT_PAGES = 9,
+    PCS_TUNE_DESC_SORT = 10,
+    PCS_TUNE_INLINE_LIST = 11,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
@@ -241,7 +261,8 @@ int pcs_gen_desc_dev(void *d_base, const uint64_t *d_off, const uint32_t *d_len,
 int pcs_flip_byte_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, uint64_t every,
                       uint64_t byte_offset, pcs_stream_t stream);
 /* Streaming-read ceiling: same load pattern as the XXH3 page kernel with the
- * hash replaced by an xor/add fold (page_size a power of two, 256..65536). */
+ * hash replaced by an xor/add fold (page_size a power of two, 256..65536;
+ * split slices for the page sizes PCS_TUNE_XXH3_SPLIT_PAGES selects). */
 int pcs_read_ceiling_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages,
                          uint64_t *d_out, pcs_stream_t stream);
 

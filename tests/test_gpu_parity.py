@@ -343,12 +343,27 @@ def test_full_size_64k_chunks_sampled():
     torch.cuda.empty_cache()
 
 
-def test_read_ceiling_runs():
-    P, n = 4096, 1000
+def _ceiling_fold(pages: np.ndarray, P: int) -> np.ndarray:
+    """What pcs_read_ceiling_dev computes: per lane (16 per slice) xor/add folds
+    of its 16-byte pieces, xor-reduced over lanes and slices."""
+    G = P // 4096 if P >= pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES) > 0 else 1
+    w = pages.view(np.uint32).reshape(-1, G, P // G // 256, 16, 4)
+    x = np.bitwise_xor.reduce(w[..., 0], axis=2).astype(np.uint64)
+    y = w[..., 1].astype(np.uint64).sum(axis=2) & 0xFFFFFFFF
+    z = np.bitwise_xor.reduce(w[..., 2], axis=2).astype(np.uint64)
+    ww = w[..., 3].astype(np.uint64).sum(axis=2) & 0xFFFFFFFF
+    r = ((x ^ z) << np.uint64(32)) | ((y + ww) & np.uint64(0xFFFFFFFF))
+    return np.bitwise_xor.reduce(r.reshape(r.shape[0], -1), axis=1)
+
+
+@pytest.mark.parametrize("P", [4096, 8192, 65536])
+def test_read_ceiling_fold(P):
+    """The roofline's read-ceiling kernel reads every byte of the layout it mirrors."""
+    n = 1000 if P <= 8192 else 70
     buf = dev_pages(P, n, 3, 0)
     out = torch.empty(n, dtype=torch.int64, device=DEV)
     pcs.read_ceiling(buf, P, n, out)
-    torch.cuda.synchronize()
+    assert np.array_equal(u64(out), _ceiling_fold(buf.cpu().numpy(), P))
 
 
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--nt", default="0,1")
     ap.add_argument("--system-hip", action="store_true")
     ap.add_argument("--x64-layouts", default="0,1")
+    ap.add_argument("--rt-batch", default="1", help="XXH3 run-time-size kernels: 1 = 4-block batches, 0 = one block")
+    ap.add_argument("--split", default="0", help="XXH3 split-page thresholds to compare (0 = group per page)")
+    ap.add_argument("--sort", default="0", help="descriptor tile sort by size (XXH3 rt batch 1 only)")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
     args = ap.parse_args()
     dev = "cuda:0"
@@ -52,7 +55,9 @@ def main():
             nbytes = total
             P = None
         else:
-            P, n = {2: (4096, 1 << 20), 4: (65536, 1 << 18), 5: (4096, 1 << 23)}[cfg]
+            # 6/7/8: 4 GiB of 8/16/32 KiB pages (not BASELINE configs; page-size sweeps)
+            P, n = {2: (4096, 1 << 20), 4: (65536, 1 << 18), 5: (4096, 1 << 23), 6: (8192, 1 << 19),
+                    7: (16384, 1 << 18), 8: (32768, 1 << 17)}[cfg]
             if args.raw_alloc:
                 hip = ctypes.CDLL("libamdhip64.so.7")
                 ptr = ctypes.c_void_p()
@@ -68,20 +73,30 @@ def main():
         for algo_name in args.algos.split(","):
             algo = pcs.XXH3_64 if algo_name == "xxh3" else pcs.XXH64
             key = pcs.TUNE_XXH3_BLOCKS_PER_CU if algo == 0 else pcs.TUNE_XXH64_BLOCKS_PER_CU
-            layouts = [int(x) for x in args.x64_layouts.split(",")] if algo == 1 else [0]
+            layouts = [int(x) for x in (args.x64_layouts if algo == 1 else args.rt_batch).split(",")]
+            splits = [int(x) for x in args.split.split(",")] if algo == 0 else [0]
+            sorts = [int(x) for x in args.sort.split(",")] if algo == 0 else [0]
             for lay in layouts:
-                for bpc in bpcs:
-                    for nt in nts:
-                        tag = f" lay={lay}" if algo == 1 else ""
-                        variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash", lay))
+                for sp in [(a, b) for a in splits for b in sorts]:
+                    for bpc in bpcs:
+                        for nt in nts:
+                            tag = (f" lay={lay}" if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
+                                   + (" sort" if sp[1] else ""))
+                            variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
+                                             (lay, sp)))
         if P in (4096, 65536):
             for nt in nts:
-                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", 0))
+                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", (1, (0, 0))))
 
         def run(v):
-            _, algo, key, bpc, nt, kind, lay = v
+            _, algo, key, bpc, nt, kind, (lay, (sp, srt)) = v
             pcs.set_tuning(key, bpc)
-            pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
+            pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, sp)
+            pcs.set_tuning(pcs.TUNE_DESC_SORT, srt)
+            if algo == 1:
+                pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
+            else:
+                pcs.set_tuning(pcs.TUNE_XXH3_RT_BATCH, lay)
             if algo == 1 and lay == 1:
                 pcs.set_tuning(pcs.TUNE_XXH64_NT_LOADS, nt)
             else:

@@ -65,7 +65,9 @@ int main() {
     std::shuffle(perm.begin(), perm.end(), rng);
     std::vector<uint8_t> ok(N);
     uint64_t fb;
+    for (int inl : {1, 0})
     for (size_t nb : {1, 16, 128, 256}) {
+        pcs_set_tuning(PCS_TUNE_INLINE_LIST, inl);
         std::vector<const void*> zp(nb), gp(nb);
         for (size_t i = 0; i < nb; ++i) {
             zp[i] = static_cast<uint8_t*>(pool) + perm[i] * P;
@@ -85,7 +87,7 @@ int main() {
             pcs_batch_wait(b);
         });
         pcs_batch_destroy(b);
-        printf("%4zu pages: zero-copy sync %6.1f us | async poll %6.1f | async wait %6.1f | staged %6.1f us\n", nb, z, a,
+        printf("inline=%d %4zu pages: zero-copy sync %6.1f us | async poll %6.1f | async wait %6.1f | staged %6.1f us\n", inl, nb, z, a,
                sub, g);
     }
     pcs_host_unregister(pool);
