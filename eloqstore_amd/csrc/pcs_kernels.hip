@@ -515,11 +515,148 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
 
 // Descriptor batch (mixed sizes).  Pages that miss the fast-path shape are
 // left to k_generic_desc.
+// Descriptor pages handled by k_xxh3_desc_split: whole 4 KiB slices, at most
+// 16 KiB (a tile of 16 pages is then at most 64 slices).
+__device__ __forceinline__ bool desc_split_ok(uint64_t off, uint32_t P) {
+    return (P % 4096u) == 0 && P >= 4096u && P <= 16384u && (off % 16u) == 0;
+}
+
+// Mixed-size descriptor batches with the split-page scheme (k_xxh3_split),
+// PCS_TUNE_DESC_SPLIT = 1.  Measured 8 % SLOWER than k_xxh3_desc on config 3
+// (6.38 vs 6.93 TB/s, profiles/r01/dsplit_lab.txt: the per-tile prefix, chain
+// and three barriers, at 3 waves per SIMD), so it is off by default:
+
+// the 4 KiB slices of a tile's 16 pages are dealt to the 16 groups in rounds,
+// 16 consecutive slices per round, so a workgroup reads 64 KiB of (packed)
+// page bytes at a time whatever the page sizes, and no group idles while a
+// neighbour walks a longer page.  Each group leaves the block sums of its
+// slice in LDS; then group i runs page i's scramble chain and merge.
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_xxh3_desc_split(const uint8_t* __restrict__ base,
+                                                        const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ len, uint64_t n,
+                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                        unsigned long long* first_bad) {
+    constexpr int kMaxSlices = 64;
+    __shared__ uint64_t S[kMaxSlices * 4][4][2];  // block sums, block 4k + i of slice k
+    __shared__ uint64_t C[kMaxSlices];            // first input word of each slice (previous block's carry)
+    __shared__ uint8_t sl_page[kMaxSlices], sl_num[kMaxSlices];
+    __shared__ uint8_t first_slice[17];
+    __shared__ uint64_t stored_w[16], tile_h[16];
+    __shared__ uint8_t tile_ok[16], tile_has[16];
+    // the lane's key set is built per phase rather than kept live across the tile
+    const int grp = threadIdx.x >> 4, p = threadIdx.x & 3;
+    const uint64_t k22 = c_keys.acc[22];
+    const uint64_t ntiles = (n + 15) / 16;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
+        if (threadIdx.x < 16) {  // slice counts and their prefix sum (lanes 0-15 of wave 0)
+            const uint64_t i = t * 16 + threadIdx.x;
+            int cnt = 0;
+            if (i < n && desc_split_ok(off[i], len[i])) cnt = (int)(len[i] / 4096u);
+            int incl = cnt;
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) {
+                const int v = __shfl_up(incl, d, 16);
+                if ((int)threadIdx.x >= d) incl += v;
+            }
+            const int excl = incl - cnt;
+            first_slice[threadIdx.x] = (uint8_t)excl;
+            if (threadIdx.x == 15) first_slice[16] = (uint8_t)incl;
+            for (int k = 0; k < cnt; ++k) {
+                sl_page[excl + k] = (uint8_t)threadIdx.x;
+                sl_num[excl + k] = (uint8_t)k;
+            }
+            tile_has[threadIdx.x] = cnt > 0;
+        }
+        __syncthreads();
+        const int total = first_slice[16];
+        for (int r = 0; r * 16 < total; ++r) {  // block-uniform trip count
+            const int k = r * 16 + grp;
+            if (k < total) {
+                const int i = sl_page[k], j = sl_num[k];
+                const uint64_t pg = t * 16 + i;
+                const uint32_t P = len[pg];
+                const u32x4* src = reinterpret_cast<const u32x4*>(base + off[pg] + 4096u * j) + (threadIdx.x & 15);
+                u32x4 d[4][4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) d[b][c] = ld16<NT>(src + b * 64 + c * 16);
+                if ((threadIdx.x & 15) == 0) {
+                    C[k] = lo64(d[0][0]);
+                    if (j == 0) stored_w[i] = lo64(d[0][0]);
+                }
+                const bool last = (j == (int)(P / 4096u) - 1);
+                const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    uint64_t Te, To;
+                    if (b < 3) xxh3_block_terms<false>(L, d[b], lo64(d[b + 1][0]), 4, Te, To);
+                    else if (!last) xxh3_block_terms<false, true>(L, d[b], 0, 4, Te, To);
+                    else xxh3_block_terms<true>(L, d[b], 0, 4, Te, To);
+                    if (L.g < 4) {
+                        S[4 * k + b][p][0] = Te;
+                        S[4 * k + b][p][1] = To;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        {  // group i: page i's chain
+            const int i = grp;
+            const uint64_t pg = t * 16 + i;
+            if (tile_has[i]) {
+                const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+                const uint32_t P = len[pg];
+                const int NB = (int)(P / 1024u) - 1, s0 = 4 * first_slice[i];
+                uint64_t Ae = L.init_e, Ao = L.init_o;
+                for (int b = 0; b < NB; ++b) {
+                    uint64_t Te = S[s0 + b][p][0], To = S[s0 + b][p][1];
+                    if ((b & 3) == 3 && p == 3) {
+                        const uint64_t cw = C[first_slice[i] + ((b + 1) >> 2)];
+                        Te += cw;
+                        To += mul32x32(cw ^ k22);
+                    }
+                    Ae = xxh3_scramble(Ae + Te, L.ks_e);
+                    Ao = xxh3_scramble(Ao + To, L.ks_o);
+                }
+                const uint64_t h = xxh3_merge(L, Ae + S[s0 + NB][p][0], Ao + S[s0 + NB][p][1], (uint64_t)(P - 8));
+                if (L.g == 0) {
+                    tile_h[i] = h;
+                    tile_ok[i] = h == stored_w[i];
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 16 && tile_has[threadIdx.x]) {
+            const uint64_t i = t * 16 + threadIdx.x;
+            const uint64_t h = tile_h[threadIdx.x];
+            if (MODE == kStamp) {
+                st_nt(reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(base) + off[i]), h);
+                if (out) st_nt(out + i, h);
+            } else {
+                if (MODE == kDigest || out) st_nt(out + i, h);
+                if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
+            }
+        }
+        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+            for (int k = 0; k < 16 && t * 16 + k < n; ++k)
+                if (tile_has[k] && !tile_ok[k]) {
+                    note_bad(first_bad, t * 16 + k);
+                    break;
+                }
+        }
+        __syncthreads();  // LDS is rewritten by the next tile
+    }
+}
+
 template <int MODE, bool NT, bool B4, bool SORT>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad) {
+                                                  unsigned long long* first_bad, int skip_split) {
     // SORT: the 16 pages of a tile are handed to the groups in order of size,
     // so the four groups of a wave mostly share one size and none idles while
     // a neighbour walks a longer page (mixed-size batches, config 3).
@@ -549,7 +686,7 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
         if (pg < n) {
             const uint64_t o = off[pg];
             const uint32_t P = len[pg];
-            if (xxh3_fast_ok(o, P)) {
+            if (xxh3_fast_ok(o, P) && !(skip_split && desc_split_ok(o, P))) {
                 const uint8_t* page = base + o;
                 uint64_t stored = 0;
                 const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
@@ -1350,13 +1487,14 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 12;
+constexpr int kTuneKeys = 13;
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
                                           /*xxh3 split pages from this size (0 = never)*/ 8192,
                                           /*descriptor tiles sorted by page size*/ 0,
-                                          /*zero-copy page list in kernel arguments*/ 1};
+                                          /*zero-copy page list in kernel arguments*/ 1,
+                                          /*descriptor pages in 4 KiB slices*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
@@ -1508,8 +1646,19 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
         // fast kernels for conforming pages, generic lanes for the rest
         if (algo == 0) {
             const unsigned grid = page_grid(n, kBlock / 16, 1);
-#define L(NT_, B4_, SORT_) \
-    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_, SORT_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
+            const int dsplit = g_tune[12].load(std::memory_order_relaxed) != 0 ? 1 : 0;
+            if (dsplit) {
+                const unsigned sgrid = (unsigned)std::min<uint64_t>((n + 15) / 16, 0x7FFFFFFFull);
+                if (use_nt())
+                    hipLaunchKernelGGL((k_xxh3_desc_split<MODE, true>), dim3(sgrid), dim3(kBlock), 0, s, base, off, len,
+                                       n, out, ok, fb);
+                else
+                    hipLaunchKernelGGL((k_xxh3_desc_split<MODE, false>), dim3(sgrid), dim3(kBlock), 0, s, base, off,
+                                       len, n, out, ok, fb);
+            }
+#define L(NT_, B4_, SORT_)                                                                                          \
+    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_, SORT_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, \
+                       fb, dsplit)
             const bool srt = g_tune[10].load(std::memory_order_relaxed) != 0;
             if (use_nt()) {
                 if (rt_batch4()) {

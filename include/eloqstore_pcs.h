@@ -224,7 +224,11 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     to the groups in order of size
  *   PCS_TUNE_INLINE_LIST          [1] zero-copy XXH3 batches of <= 256 pages
  *                                     pass the page list in the kernel
- *                                     arguments (0 = read it from host memory) */
+ *                                     arguments (0 = read it from host memory)
+ *   PCS_TUNE_DESC_SPLIT           [0] 1 = XXH3 descriptor pages of 4, 8, 12 or
+ *                                     16 KiB are hashed in 4 KiB slices dealt
+ *                                     to the groups round by round; 0 = one
+ *                                     group walks each page (measured faster) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -237,6 +241,7 @@ enum pcs_tune_key {
     PCS_TUNE_XXH3_SPLIT_PAGES = 9,
     PCS_TUNE_DESC_SORT = 10,
     PCS_TUNE_INLINE_LIST = 11,
+    PCS_TUNE_DESC_SPLIT = 12,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -185,6 +185,54 @@ def test_desc_odd_shapes(algo):
     assert okh[lens < 8].sum() == 0  # header-less pages never validate
 
 
+@pytest.mark.parametrize("dsplit", [0, 1])
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+def test_desc_mixed_wide(algo, dsplit):
+    """Many pages of many sizes in random order: every kernel split of the
+    descriptor path (4 KiB-slice tiles, run-time-size groups, generic lanes)
+    sees neighbours of other shapes."""
+    rng = np.random.default_rng(0xD35C)
+    sizes = np.array([4096, 8192, 12288, 16384, 20480, 32768, 5120, 1280, 256, 4104, 65536, 100], dtype=np.uint32)
+    n = 3000
+    lens = sizes[rng.integers(0, len(sizes), size=n)]
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i, L in enumerate(lens):
+        pos += 8 if rng.random() < 0.05 else 0  # a few 8-byte-misaligned pages
+        offs[i] = pos
+        pos += int(L)
+        pos = (pos + 15) // 16 * 16 if rng.random() < 0.95 else pos
+    host = rng.integers(0, 256, size=pos + 64, dtype=np.uint8)
+    base = torch.from_numpy(host).to(DEV)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+    want = np.array([oracle.pages_digest(host[int(o):int(o) + int(L)], int(L), algo)[0] for o, L in zip(offs, lens)],
+                    dtype=np.uint64)
+    saved = pcs.get_tuning(pcs.TUNE_DESC_SPLIT)
+    pcs.set_tuning(pcs.TUNE_DESC_SPLIT, dsplit)
+    try:
+        _desc_mixed_wide_checks(base, d_off, d_len, n, algo, offs, lens, want)
+    finally:
+        pcs.set_tuning(pcs.TUNE_DESC_SPLIT, saved)
+
+
+def _desc_mixed_wide_checks(base, d_off, d_len, n, algo, offs, lens, want):
+    got = u64(pcs.desc_digest(base, d_off, d_len, n, algo))
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
+    pcs.desc_stamp(base, d_off, d_len, n, algo)
+    h2 = base.cpu().numpy()
+    stamped = np.array([h2[int(o):int(o) + 8].view(np.uint64)[0] for o in offs], dtype=np.uint64)
+    assert np.array_equal(stamped, want)
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert ok.cpu().numpy().all() and int(u64(fb)[0]) == 2**64 - 1
+    bad = [7, 1500, 2999]
+    for i in bad:
+        h2[int(offs[i]) + int(lens[i]) // 2] ^= 0x10
+    base.copy_(torch.from_numpy(h2))
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert list(np.flatnonzero(ok.cpu().numpy() == 0)) == bad and int(u64(fb)[0]) == 7
+
+
 def test_raw_ranges_sweep(golden):
     sw = golden["sweep"]
     buf = splitmix_words(sw["seed"], sw["page_index"], sw["words"]).view(np.uint8)

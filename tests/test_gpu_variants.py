@@ -31,12 +31,13 @@ VARIANTS = {
     "split_16k": {pcs.TUNE_XXH3_SPLIT_PAGES: 16384},
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "desc_sort": {pcs.TUNE_DESC_SORT: 1},
+    "desc_split": {pcs.TUNE_DESC_SPLIT: 1},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = list(range(1, 12))
+    keys = list(range(1, 13))
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -68,7 +69,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_quad",
-                                   "desc_sort"],
+                                   "desc_sort", "desc_split"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):

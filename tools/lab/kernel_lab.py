@@ -35,8 +35,9 @@ def main():
     ap.add_argument("--system-hip", action="store_true")
     ap.add_argument("--x64-layouts", default="0,1")
     ap.add_argument("--rt-batch", default="1", help="XXH3 run-time-size kernels: 1 = 4-block batches, 0 = one block")
-    ap.add_argument("--split", default="0", help="XXH3 split-page thresholds to compare (0 = group per page)")
+    ap.add_argument("--split", default="8192", help="XXH3 split-page thresholds to compare (0 = group per page)")
     ap.add_argument("--sort", default="0", help="descriptor tile sort by size (XXH3 rt batch 1 only)")
+    ap.add_argument("--dsplit", default="1", help="XXH3 descriptor pages in 4 KiB slices (1) or not (0)")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
     args = ap.parse_args()
     dev = "cuda:0"
@@ -75,24 +76,25 @@ def main():
             key = pcs.TUNE_XXH3_BLOCKS_PER_CU if algo == 0 else pcs.TUNE_XXH64_BLOCKS_PER_CU
             layouts = [int(x) for x in (args.x64_layouts if algo == 1 else args.rt_batch).split(",")]
             splits = [int(x) for x in args.split.split(",")] if algo == 0 else [0]
-            sorts = [int(x) for x in args.sort.split(",")] if algo == 0 else [0]
+            sorts = [(a, b) for a in [int(x) for x in args.sort.split(",")] for b in [int(x) for x in args.dsplit.split(",")]] if algo == 0 else [(0, 1)]
             for lay in layouts:
                 for sp in [(a, b) for a in splits for b in sorts]:
                     for bpc in bpcs:
                         for nt in nts:
                             tag = (f" lay={lay}" if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
-                                   + (" sort" if sp[1] else ""))
+                                   + (" sort" if sp[1][0] else "") + ("" if sp[1][1] else " nodsplit"))
                             variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
                                              (lay, sp)))
         if P in (4096, 65536):
             for nt in nts:
-                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", (1, (0, 0))))
+                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", (1, (8192, (0, 1)))))
 
         def run(v):
-            _, algo, key, bpc, nt, kind, (lay, (sp, srt)) = v
+            _, algo, key, bpc, nt, kind, (lay, (sp, (srt, dsp))) = v
             pcs.set_tuning(key, bpc)
-            pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, sp)
+            pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, sp if sp >= 0 else 0)
             pcs.set_tuning(pcs.TUNE_DESC_SORT, srt)
+            pcs.set_tuning(pcs.TUNE_DESC_SPLIT, dsp)
             if algo == 1:
                 pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
             else:
