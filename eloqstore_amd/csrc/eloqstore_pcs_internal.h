@@ -8,8 +8,8 @@
 namespace pcs {
 
 // mode: 0 digest, 1 validate, 2 stamp.  algo: 0 XXH3-64, 1 XXH64.
-// Fixed-stride pages; returns hipErrorNotSupported when the shape needs the
-// descriptor path (unaligned base, odd page size).
+// Fixed-stride pages, any shape (odd shapes run as a descriptor batch built
+// on the device).
 hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t* out,
                      uint8_t* ok, unsigned long long* first_bad, hipStream_t s);
 
@@ -41,6 +41,10 @@ hipError_t run_flip(uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t eve
                     hipStream_t s);
 // ManifestBuilder::CalcChecksum over a device-resident content buffer
 hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hipStream_t s);
+// Event-fenced device scratch (see ScratchPool in pcs_kernels.hip): the
+// buffer is reused only after the work queued on `s` at release completes.
+hipError_t scratch_acquire(size_t bytes, void** out, int* id);
+hipError_t scratch_release(int id, hipStream_t s);
 int set_tuning(int key, int64_t value);
 int64_t get_tuning(int key);
 hipError_t run_read_ceiling(const uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t* out, hipStream_t s);

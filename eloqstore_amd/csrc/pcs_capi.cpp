@@ -68,28 +68,8 @@ int pages_common(int mode, const void* d_pages, uint64_t P, uint64_t n, int algo
     }
     if (n == 0) return PCS_OK;
     auto* fb = reinterpret_cast<unsigned long long*>(d_first_bad);
-    hipError_t e = pcs::run_pages(mode, algo, static_cast<const uint8_t*>(d_pages), P, n, d_out, d_ok, fb, s);
-    if (e != hipErrorNotSupported) return finish(e, "page kernel launch");
-    (void)hipGetLastError();
-    // Odd shape: descriptors (off = i*P, len = P) in a temporary device array.
-    uint64_t* d_off = nullptr;
-    uint32_t* d_len = nullptr;
-    if ((e = hipMallocAsync(reinterpret_cast<void**>(&d_off), n * 8, s)) != hipSuccess) return hip_fail(e, "hipMallocAsync");
-    if ((e = hipMallocAsync(reinterpret_cast<void**>(&d_len), n * 4, s)) != hipSuccess) {
-        (void)hipFreeAsync(d_off, s);
-        return hip_fail(e, "hipMallocAsync");
-    }
-    std::vector<uint64_t> off(n);
-    std::vector<uint32_t> len(n, (uint32_t)P);
-    for (uint64_t i = 0; i < n; ++i) off[i] = i * P;
-    e = hipMemcpyAsync(d_off, off.data(), n * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_len, len.data(), n * 4, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = pcs::run_desc(mode, algo, static_cast<const uint8_t*>(d_pages), d_off, d_len, n, 8, 0, d_out, d_ok, fb, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);  // host vectors must outlive the copies
-    (void)hipFreeAsync(d_off, s);
-    (void)hipFreeAsync(d_len, s);
-    return finish(e, "descriptor fallback");
+    return finish(pcs::run_pages(mode, algo, static_cast<const uint8_t*>(d_pages), P, n, d_out, d_ok, fb, s),
+                  "page kernel launch");
 }
 
 int desc_common(int mode, const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n, int algo,
@@ -430,14 +410,6 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
                            s.stream);
         if (e == hipSuccess)
             e = pcs::run_pages(mode == 1 ? 1 : 0, algo, s.d_pages, P, cnt, s.d_dig, s.d_ok, nullptr, s.stream);
-        if (e == hipErrorNotSupported) {
-            (void)hipGetLastError();
-            // staging is 256-byte aligned, so only an odd page size lands here
-            rc = pages_common(mode == 1 ? 1 : 0, s.d_pages, P, cnt, algo, s.d_dig, s.d_ok, nullptr,
-                              reinterpret_cast<pcs_stream_t>(s.stream));
-            if (rc) break;
-            e = hipSuccess;
-        }
         if (e == hipSuccess) {
             if (mode == 1) e = hipMemcpyAsync(s.h_ok, s.d_ok, cnt, hipMemcpyDeviceToHost, s.stream);
             else e = hipMemcpyAsync(s.h_dig, s.d_dig, cnt * 8, hipMemcpyDeviceToHost, s.stream);
@@ -463,16 +435,16 @@ int manifest_host(const void* content, uint64_t len, uint64_t* out) {
     hipStream_t s = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
-    uint8_t* d = nullptr;
-    uint64_t* d_out = nullptr;
-    e = hipMallocAsync(reinterpret_cast<void**>(&d_out), 8, s);
-    if (e == hipSuccess && len) e = hipMallocAsync(reinterpret_cast<void**>(&d), len, s);
+    void* buf = nullptr;  // [digest word | content]
+    int id = -1;
+    e = pcs::scratch_acquire(8 + len, &buf, &id);
+    uint64_t* d_out = static_cast<uint64_t*>(buf);
+    uint8_t* d = static_cast<uint8_t*>(buf) + 8;
     if (e == hipSuccess && len) e = hipMemcpyAsync(d, content, len, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = pcs::run_manifest(d, len, d_out, s);
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (d) (void)hipFreeAsync(d, s);
-    if (d_out) (void)hipFreeAsync(d_out, s);
+    if (id >= 0) (void)pcs::scratch_release(id, s);
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
     return finish(e, "manifest checksum");
@@ -753,15 +725,6 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
     e = hipMemcpyAsync(b->d_pages, direct ? pages[0] : b->h_pages, n * P, hipMemcpyHostToDevice, s);
     const int kmode = mode == PCS_BATCH_VALIDATE ? 1 : 0;
     if (e == hipSuccess) e = pcs::run_pages(kmode, algo, b->d_pages, P, n, b->d_dig, b->d_ok, nullptr, s);
-    if (e == hipErrorNotSupported) {
-        (void)hipGetLastError();
-        if (int rc = pages_common(kmode, b->d_pages, P, n, algo, b->d_dig, b->d_ok, nullptr,
-                                  reinterpret_cast<pcs_stream_t>(s))) {
-            b->state = -1;
-            return rc;
-        }
-        e = hipSuccess;
-    }
     if (e == hipSuccess)
         e = kmode ? hipMemcpyAsync(b->h_ok, b->d_ok, n, hipMemcpyDeviceToHost, s)
                   : hipMemcpyAsync(b->h_dig, b->d_dig, n * 8, hipMemcpyDeviceToHost, s);

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 namespace pcs {
 
@@ -1479,6 +1480,102 @@ unsigned grid_for(uint64_t units, unsigned units_per_block, unsigned blocks_per_
 constexpr unsigned kBlock = 256;
 constexpr unsigned kBlocksPerCu = 8;  // grid-stride cap for the auxiliary kernels
 
+// Device scratch for multi-kernel operations (two-pass stamp, manifest
+// chunk tables), fenced by events instead of the stream-ordered allocator.
+// hipMallocAsync / hipFreeAsync scratch was measured to lose writes: a stamp
+// enqueued while the GPU was still busy left 7 % of the page headers zero
+// (tools/lab/read_lab.hip "stamp", profiles/r01/stamp_lab.txt).  A buffer
+// here is handed out only when the event recorded after its last use has
+// completed, so concurrent streams and host threads never share one in
+// flight.  Buffers are kept for reuse (bounded by the number of operations
+// in flight at once).
+class ScratchPool {
+public:
+    hipError_t acquire(size_t bytes, void** out, int* id) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        std::lock_guard<std::mutex> lk(mu_);
+        int empty = -1;
+        for (size_t i = 0; i < bufs_.size(); ++i) {
+            Buf& b = bufs_[i];
+            if (b.dev != dev || b.busy) continue;
+            if (!b.p) {
+                empty = (int)i;
+                continue;
+            }
+            const hipError_t q = hipEventQuery(b.done);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) return q;
+            if (b.bytes < bytes) {
+                if (b.bytes > kKeepBytes) {  // idle and oversized: give it back
+                    (void)hipFree(b.p);
+                    b.p = nullptr;
+                    b.bytes = 0;
+                    empty = (int)i;
+                }
+                continue;
+            }
+            b.busy = true;
+            *out = b.p;
+            *id = (int)i;
+            return hipSuccess;
+        }
+        Buf b;
+        b.dev = dev;
+        b.bytes = std::max<size_t>(bytes, 1u << 20);
+        if ((e = hipMalloc(&b.p, b.bytes)) != hipSuccess) return e;
+        b.busy = true;
+        if (empty >= 0) {
+            b.done = bufs_[(size_t)empty].done;
+            bufs_[(size_t)empty] = b;
+            *id = empty;
+        } else {
+            if ((e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming)) != hipSuccess) {
+                (void)hipFree(b.p);
+                return e;
+            }
+            bufs_.push_back(b);
+            *id = (int)bufs_.size() - 1;
+        }
+        *out = b.p;
+        return hipSuccess;
+    }
+    // The buffer becomes reusable once the work queued on s so far completes.
+    hipError_t release(int id, hipStream_t s) {
+        std::lock_guard<std::mutex> lk(mu_);
+        Buf& b = bufs_[(size_t)id];
+        const hipError_t e = hipEventRecord(b.done, s);
+        b.busy = false;
+        return e;
+    }
+
+private:
+    static constexpr size_t kKeepBytes = 256u << 20;  // larger idle buffers are freed, not kept
+    struct Buf {
+        void* p = nullptr;
+        size_t bytes = 0;
+        hipEvent_t done = nullptr;
+        int dev = 0;
+        bool busy = false;
+    };
+    std::mutex mu_;
+    std::vector<Buf> bufs_;
+};
+ScratchPool g_scratch;
+
+// RAII lease of a scratch buffer for the work enqueued on one stream.
+struct ScratchLease {
+    void* p = nullptr;
+    int id = -1;
+    hipStream_t s;
+    explicit ScratchLease(hipStream_t st) : s(st) {}
+    hipError_t get(size_t bytes) { return g_scratch.acquire(bytes, &p, &id); }
+    ~ScratchLease() {
+        if (id >= 0) (void)g_scratch.release(id, s);
+    }
+};
+
 bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) == 0; }
 
 }  // namespace
@@ -1591,7 +1688,11 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
             // kernel), then one scattered 8-byte write per page
             uint64_t* dig = out;
             hipError_t e = hipSuccess;
-            if (!dig) e = hipMallocAsync(reinterpret_cast<void**>(&dig), n * 8, s);
+            ScratchLease scratch(s);
+            if (!dig) {
+                e = scratch.get(n * 8);
+                dig = static_cast<uint64_t*>(scratch.p);
+            }
             if (e == hipSuccess)
                 e = use_nt() ? launch_xxh3_pages<kDigest, true>(P, pages, n, dig, nullptr, nullptr, s)
                              : launch_xxh3_pages<kDigest, false>(P, pages, n, dig, nullptr, nullptr, s);
@@ -1600,7 +1701,6 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
                                    const_cast<uint8_t*>(pages), P, n, dig);
                 e = hipGetLastError();
             }
-            if (dig && dig != out) (void)hipFreeAsync(dig, s);
             return e;
         }
         return use_nt() ? launch_xxh3_pages<MODE, true>(P, pages, n, out, ok, fb, s)
@@ -1628,14 +1728,36 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
     return hipErrorNotSupported;  // caller falls back to the descriptor path
 }
 
-hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
-                     unsigned long long* fb, hipStream_t s) {
-    switch (mode) {
-        case kDigest: return pages_impl<kDigest>(algo, pages, P, n, out, ok, fb, s);
-        case kValidate: return pages_impl<kValidate>(algo, pages, P, n, out, ok, fb, s);
-        default: return pages_impl<kStamp>(algo, pages, P, n, out, ok, fb, s);
+__global__ void k_uniform_desc(uint64_t P, uint64_t n, uint64_t* __restrict__ off, uint32_t* __restrict__ len) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        off[i] = i * P;
+        len[i] = (uint32_t)P;
     }
 }
+
+hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
+                     unsigned long long* fb, hipStream_t s) {
+    hipError_t e;
+    switch (mode) {
+        case kDigest: e = pages_impl<kDigest>(algo, pages, P, n, out, ok, fb, s); break;
+        case kValidate: e = pages_impl<kValidate>(algo, pages, P, n, out, ok, fb, s); break;
+        default: e = pages_impl<kStamp>(algo, pages, P, n, out, ok, fb, s); break;
+    }
+    if (e != hipErrorNotSupported) return e;
+    // Odd shape (unaligned base, page size off the fast kernels): the same
+    // pages as a descriptor batch (off = i * P, len = P) built on the device.
+    ScratchLease scratch(s);
+    if ((e = scratch.get(n * 12)) != hipSuccess) return e;
+    uint64_t* off = static_cast<uint64_t*>(scratch.p);
+    uint32_t* len = reinterpret_cast<uint32_t*>(off + n);
+    hipLaunchKernelGGL(k_uniform_desc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, off, len);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return run_desc(mode, algo, pages, off, len, n, 8, 0, out, ok, fb, s);
+}
+
+hipError_t scratch_acquire(size_t bytes, void** out, int* id) { return g_scratch.acquire(bytes, out, id); }
+hipError_t scratch_release(int id, hipStream_t s) { return g_scratch.release(id, s); }
 
 template <int MODE>
 static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
@@ -1712,13 +1834,13 @@ hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hip
     constexpr uint64_t kChunk = 1u << 20;  // kCheckSumBatchSize, root_meta.cpp:157
     if (len == 0) return hipMemsetAsync(out, 0, 8, s);
     const uint64_t n = (len + kChunk - 1) / kChunk;
-    uint64_t* off = nullptr;
-    uint32_t* ln = nullptr;
-    uint64_t* h = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&off), n * 8, s);
-    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&ln), n * 4, s);
-    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&h), n * 8, s);
-    if (e == hipSuccess) {
+    ScratchLease scratch(s);  // chunk offsets, lengths and digests
+    hipError_t e = scratch.get(n * 20);
+    if (e != hipSuccess) return e;
+    uint64_t* off = static_cast<uint64_t*>(scratch.p);
+    uint64_t* h = off + n;
+    uint32_t* ln = reinterpret_cast<uint32_t*>(h + n);
+    {
         hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, len, kChunk, n, off, ln);
         e = hipGetLastError();
     }
@@ -1727,9 +1849,6 @@ hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hip
         hipLaunchKernelGGL(k_manifest_fold, dim3(1), dim3(64), 0, s, h, n, out);
         e = hipGetLastError();
     }
-    if (off) (void)hipFreeAsync(off, s);
-    if (ln) (void)hipFreeAsync(ln, s);
-    if (h) (void)hipFreeAsync(h, s);
     return e;
 }
 

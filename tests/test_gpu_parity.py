@@ -571,3 +571,29 @@ def test_host_api_concurrent_threads():
     for t in th:
         t.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("use_side_stream", [False, True])
+def test_stamp_while_gpu_busy(use_side_stream):
+    """Two-pass stamp and the manifest path enqueued while the GPU is still
+    busy with earlier work: their device scratch must not be reused or
+    released before the queued kernels ran (regression: stream-ordered
+    scratch lost 7 % of the headers, profiles/r01/stamp_lab.txt)."""
+    P, n = 4096, 1 << 18
+    buf = dev_pages(P, n, 0x5EED0002, 0)
+    want = pcs.pages_digest(buf, P, n).clone()
+    stream = torch.cuda.Stream() if use_side_stream else torch.cuda.current_stream()
+    content = bytes(np.random.default_rng(3).integers(0, 256, size=(3 << 20) + 77, dtype=np.uint8))
+    with torch.cuda.stream(stream):
+        for _ in range(6):
+            torch.cuda._sleep(3_000_000)  # keep the GPU busy while we enqueue
+            buf.view(-1, P)[:, :8].zero_()
+            pcs.pages_stamp(buf, P, n, stream=stream)
+        stream.synchronize()
+    stored = buf.view(-1, P)[:, :8].contiguous().view(torch.int64).reshape(-1)
+    assert torch.equal(stored, want)
+    ok, fb = pcs.pages_validate(buf, P, n)
+    assert int(ok.sum()) == n
+    for _ in range(3):
+        torch.cuda._sleep(3_000_000)
+        assert pcs.manifest_checksum_host(content) == oracle.manifest_checksum(content)

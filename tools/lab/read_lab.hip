@@ -284,12 +284,143 @@ __global__ __launch_bounds__(256) void k_group16_big(const uint8_t* __restrict__
     }
 }
 
+// Stamp pass-2 variants: write each page's 8-byte digest into its header.
+// W = bytes written per page (8/16/32: from the digest + zeros would corrupt,
+// so W > 8 re-reads the line first: read W bytes, patch 8, write W).
+template <int W, bool NTST>
+__global__ __launch_bounds__(256) void k_scatter(uint8_t* __restrict__ pages, uint64_t P, uint64_t n,
+                                                 const uint64_t* __restrict__ dig) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t* dst = reinterpret_cast<uint64_t*>(pages + i * P);
+    if constexpr (W == 8) {
+        if constexpr (NTST) __builtin_nontemporal_store(dig[i], dst);
+        else *dst = dig[i];
+    } else {
+        uint64_t line[W / 8];
+#pragma unroll
+        for (int k = 0; k < W / 8; ++k) line[k] = dst[k];
+        line[0] = dig[i];
+#pragma unroll
+        for (int k = 0; k < W / 8; ++k) {
+            if constexpr (NTST) __builtin_nontemporal_store(line[k], dst + k);
+            else dst[k] = line[k];
+        }
+    }
+}
+
+// one wave per 64 pages, but lanes cooperate: lane l writes 8 B of page
+// (base + l / (W/8)) so each page's W-byte header is one contiguous store
+// group (W > 8 re-reads the header first).
+template <int W>
+__global__ __launch_bounds__(256) void k_scatter_coop(uint8_t* __restrict__ pages, uint64_t P, uint64_t n,
+                                                      const uint64_t* __restrict__ dig) {
+    constexpr int L = W / 8;  // lanes per page
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i = t / L;
+    const int k = (int)(t % L);
+    if (i >= n) return;
+    uint64_t* dst = reinterpret_cast<uint64_t*>(pages + i * P) + k;
+    const uint64_t v = k == 0 ? dig[i] : *dst;
+    __builtin_nontemporal_store(v, dst);
+}
+
+static int main_stamp(int rounds) {
+    const uint64_t P = 4096, n = 1 << 20, bytes = n * P;
+    uint8_t* pages;
+    uint64_t* dig;
+    CK(hipMalloc(&pages, bytes));
+    CK(hipMalloc(&dig, n * 8));
+    if (pcs_gen_pages_dev(pages, P, n, 0x5EED0002, 0, nullptr)) std::exit(2);
+    if (pcs_pages_digest_dev(pages, P, n, 0, dig, nullptr)) std::exit(2);
+    CK(hipDeviceSynchronize());
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    struct V { std::string name; std::function<void(hipStream_t)> run; std::vector<float> ms; };
+    std::vector<V> vs;
+    auto add = [&](std::string name, std::function<void(hipStream_t)> f) { vs.push_back({name, f, {}}); };
+    const unsigned g1 = (unsigned)((n + 255) / 256);
+    add("scatter 8B plain", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter<8, false>), dim3(g1), dim3(256), 0, st, pages, P, n, dig); });
+    add("scatter 8B nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter<8, true>), dim3(g1), dim3(256), 0, st, pages, P, n, dig); });
+    add("scatter 32B rmw nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter<32, true>), dim3(g1), dim3(256), 0, st, pages, P, n, dig); });
+    add("scatter 64B rmw nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter<64, true>), dim3(g1), dim3(256), 0, st, pages, P, n, dig); });
+    add("scatter 64B rmw plain", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter<64, false>), dim3(g1), dim3(256), 0, st, pages, P, n, dig); });
+    add("coop 32B", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter_coop<32>), dim3(g1 * 4), dim3(256), 0, st, pages, P, n, dig); });
+    add("coop 64B", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter_coop<64>), dim3(g1 * 8), dim3(256), 0, st, pages, P, n, dig); });
+    add("coop 128B", [=](hipStream_t st) { hipLaunchKernelGGL((k_scatter_coop<128>), dim3(g1 * 16), dim3(256), 0, st, pages, P, n, dig); });
+    add("PRODUCT pcs_pages_stamp_dev (two-pass)", [=](hipStream_t st) { pcs_pages_stamp_dev(pages, P, n, 0, (pcs_stream_t)st); });
+    add("PRODUCT pcs_pages_digest_dev", [=](hipStream_t st) { pcs_pages_digest_dev(pages, P, n, 0, dig, (pcs_stream_t)st); });
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    uint8_t* okd;
+    uint64_t* fbd;
+    CK(hipMalloc(&okd, n));
+    CK(hipMalloc(&fbd, 8));
+    for (auto& v : vs) {  // warm, and check every variant leaves all pages valid
+        v.run(s);
+        CK(hipStreamSynchronize(s));
+        if (pcs_pages_validate_dev(pages, P, n, 0, okd, fbd, (pcs_stream_t)s)) std::exit(2);
+        uint64_t f = 0;
+        CK(hipMemcpyAsync(&f, fbd, 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        std::printf("after %-38s first_bad = %s\n", v.name.c_str(), f == ~0ull ? "none" : std::to_string(f).c_str());
+    }
+    for (int r = 0; r < rounds; ++r)
+        for (auto& v : vs) {
+            hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 200000LL);
+            CK(hipEventRecord(a, s));
+            v.run(s);
+            CK(hipEventRecord(b, s));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.ms.push_back(ms);
+            if (r < 2) {
+                if (pcs_pages_validate_dev(pages, P, n, 0, okd, fbd, (pcs_stream_t)s)) std::exit(2);
+                uint64_t f = 0;
+                CK(hipMemcpyAsync(&f, fbd, 8, hipMemcpyDeviceToHost, s));
+                CK(hipStreamSynchronize(s));
+                if (f != ~0ull) std::printf("round %d after %s: first_bad = %llu\n", r, v.name.c_str(), (unsigned long long)f);
+            }
+        }
+    CK(hipGetLastError());
+    // the pages must still validate after all the header rewrites
+    uint8_t* ok;
+    uint64_t* fb;
+    CK(hipMalloc(&ok, n));
+    CK(hipMalloc(&fb, 8));
+    if (pcs_pages_validate_dev(pages, P, n, 0, ok, fb, (pcs_stream_t)s)) std::exit(2);
+    uint64_t fbh = 0;
+    CK(hipMemcpyAsync(&fbh, fb, 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (fbh != ~0ull) {  // which pages, and what do their headers hold?
+        std::vector<uint8_t> okh(n);
+        CK(hipMemcpy(okh.data(), ok, n, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t k = 0; k < n; ++k) bad += okh[k] == 0;
+        uint64_t hdr = 0, d = 0;
+        CK(hipMemcpy(&hdr, pages + fbh * P, 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&d, dig + fbh, 8, hipMemcpyDeviceToHost));
+        std::printf("bad pages: %zu; page %llu header %016llx dig %016llx\n", bad, (unsigned long long)fbh,
+                    (unsigned long long)hdr, (unsigned long long)d);
+    }
+    std::printf("validate after rewrites: first_bad = %s\n", fbh == ~0ull ? "none" : std::to_string(fbh).c_str());
+    std::printf("%-40s %9s\n", "variant (1 M x 4 KiB headers)", "med_us");
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        std::printf("%-40s %9.1f\n", v.name.c_str(), v.ms[v.ms.size() / 2] * 1e3);
+    }
+    return 0;
+}
+
 struct Variant;
 static int main_big(int rounds);
 
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
     if (argc > 2 && std::string(argv[2]) == "big") return main_big(rounds);
+    if (argc > 2 && std::string(argv[2]) == "stamp") return main_stamp(rounds);
     const uint64_t P = 4096, n = 1 << 20, bytes = n * P;
     uint8_t* pages;
     uint64_t* out;
