@@ -432,9 +432,12 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 int manifest_host(const void* content, uint64_t len, uint64_t* out) {
     if (int rc = require_device()) return rc;
     if (!out || (len && !content)) return fail(PCS_ERR_INVALID, "null pointer");
-    hipStream_t s = nullptr;
-    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    Slot& slot = t_ctx[dev].slot[0];  // the calling thread's stream on this device
+    if (int rc = ensure_slot(slot, 0, 1)) return rc;
+    hipStream_t s = slot.stream;
     void* buf = nullptr;  // [digest word | content]
     int id = -1;
     e = pcs::scratch_acquire(8 + len, &buf, &id);
@@ -445,8 +448,7 @@ int manifest_host(const void* content, uint64_t len, uint64_t* out) {
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (id >= 0) (void)pcs::scratch_release(id, s);
-    (void)hipStreamSynchronize(s);
-    (void)hipStreamDestroy(s);
+    if (e != hipSuccess) (void)hipStreamSynchronize(s);  // nothing of this call left in flight
     return finish(e, "manifest checksum");
 }
 

@@ -1340,6 +1340,91 @@ __global__ __launch_bounds__(256) void k_xxh3_long(const uint8_t* __restrict__ b
 
 // Manifest record aggregate (ManifestBuilder::CalcChecksum, root_meta.cpp:150-174):
 // chunk digests folded serially, agg = rotl(agg, 1) ^ h; agg *= 0x9e3779b97f4a7c15.
+// ---------------------------------------------------------------------------
+// Manifest checksum, wide form: few long chunks (ManifestBuilder::CalcChecksum,
+// root_meta.cpp:150-174, 1 MiB per chunk)
+// ---------------------------------------------------------------------------
+// One workgroup per chunk (k_xxh3_long) leaves a small manifest on a handful
+// of CUs: a 1 MiB record took 121 us.  Here the block sums of all chunks are
+// computed by 16-block windows spread over the whole GPU (k_manifest_sums),
+// then one workgroup per chunk loads its sums into LDS and runs the serial
+// scramble chain and the tail (k_manifest_chain).  The chain itself
+// (P/1024 - 1 dependent 64x32-bit scrambles) is the floor: ~20-30 us per
+// 1 MiB chunk.
+constexpr uint32_t kManifestChunk = 1u << 20;  // kCheckSumBatchSize, root_meta.cpp:157
+constexpr int kChunkBlocks = kManifestChunk / 1024;
+// Above 256 chunks the per-chunk workgroups fill the GPU and the wide form's
+// extra block-sum traffic loses (1 GiB: 380 vs 332 us, profiles/r01/long_lab.txt).
+constexpr uint64_t kWideMaxChunks = 256;
+
+__device__ __forceinline__ uint32_t manifest_chunk_len(uint64_t total, uint64_t c) {
+    return (uint32_t)min((uint64_t)kManifestChunk, total - c * kManifestChunk);
+}
+
+__global__ __launch_bounds__(256) void k_manifest_sums(const uint8_t* __restrict__ content, uint64_t total,
+                                                      uint64_t* __restrict__ S) {
+    const uint64_t c = blockIdx.y;
+    const uint32_t L = manifest_chunk_len(total, c);
+    if (L < kLongMin) return;  // a short last chunk is hashed whole by the chain kernel
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint32_t nb = (L - 1) / 1024;
+    const uint32_t b = blockIdx.x * 16 + grp;
+    if (b >= nb) return;
+    const uint64_t* in = reinterpret_cast<const uint64_t*>(content + c * kManifestChunk);
+    const uint64_t T = xxh3_long_block(in + (size_t)b * 128, g, 16);
+    if (g < 8) S[(c * kChunkBlocks + b) * 8 + g] = T;
+}
+
+__global__ __launch_bounds__(256) void k_manifest_chain(const uint8_t* __restrict__ content, uint64_t total,
+                                                       const uint64_t* __restrict__ S, uint64_t* __restrict__ h) {
+    __shared__ uint64_t sums[kChunkBlocks][8];
+    const uint64_t c = blockIdx.x;
+    const uint32_t L = manifest_chunk_len(total, c);
+    const uint8_t* in8 = content + c * kManifestChunk;
+    const int tid = threadIdx.x, g = tid & 15;
+    if (L < kLongMin) {
+        if (tid == 0) h[c] = xxh3_any(in8, L);
+        return;
+    }
+    const uint32_t nb = (L - 1) / 1024;
+    const u32x4* src = reinterpret_cast<const u32x4*>(S + c * kChunkBlocks * 8);
+    u32x4* dst = reinterpret_cast<u32x4*>(&sums[0][0]);
+    for (uint32_t i = tid; i < nb * 4; i += blockDim.x) dst[i] = src[i];  // nb blocks x 64 B
+    __syncthreads();
+    if (tid >= 64) return;
+    uint64_t acc = tid < 8 ? c_init_acc[tid] : 0;
+    if (tid < 8) {
+        const uint64_t key = c_keys.scr[tid];
+        uint32_t b = 0;
+        for (; b + 8 <= nb; b += 8) {  // sums do not depend on acc: read 8 ahead
+            uint64_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = sums[b + k][tid];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc = xxh3_scramble(acc + v[k], key);
+        }
+        for (; b < nb; ++b) acc = xxh3_scramble(acc + sums[b][tid], key);
+    }
+    if (tid < 16) {  // tail block, last stripe and merge, as in k_xxh3_long
+        const uint64_t* in = reinterpret_cast<const uint64_t*>(in8);
+        const int nst = (int)(((L - 1) - 1024 * nb) / 64);
+        uint64_t T = xxh3_long_block(in + (size_t)nb * 128, g, nst);
+        uint64_t M = 0, R = 0;
+        if (g < 8) {
+            const uint64_t v = ld64(in8 + L - 64 + 8 * g);
+            M = mul32x32(v ^ c_keys.last[g]);
+            R = v;
+        }
+        T += M + dpp64<kQuadSwap1>(R);
+        acc += T;
+        const uint64_t nxt = dpp64<kRowRor15>(acc);
+        uint64_t m = (g < 8 && (g & 1) == 0) ? mul_fold64(acc ^ c_keys.merge[g], nxt ^ c_keys.merge[g + 1]) : 0;
+        m += dpp64<kRowRor2>(m);
+        m += dpp64<kRowRor4>(m);
+        if (g == 6) h[c] = xxh3_avalanche((uint64_t)L * kP64_1 + m);
+    }
+}
+
 __global__ void k_manifest_fold(const uint64_t* __restrict__ chunk_h, uint64_t nchunks, uint64_t* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     uint64_t agg = 0;
@@ -1584,14 +1669,15 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 13;
+constexpr int kTuneKeys = 14;
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
                                           /*xxh3 split pages from this size (0 = never)*/ 8192,
                                           /*descriptor tiles sorted by page size*/ 0,
                                           /*zero-copy page list in kernel arguments*/ 1,
-                                          /*descriptor pages in 4 KiB slices*/ 0};
+                                          /*descriptor pages in 4 KiB slices*/ 0,
+                                          /*manifest: wide block sums + chain kernel*/ 1};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
@@ -1831,9 +1917,23 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
 }
 
 hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hipStream_t s) {
-    constexpr uint64_t kChunk = 1u << 20;  // kCheckSumBatchSize, root_meta.cpp:157
+    constexpr uint64_t kChunk = kManifestChunk;
     if (len == 0) return hipMemsetAsync(out, 0, 8, s);
     const uint64_t n = (len + kChunk - 1) / kChunk;
+    if (n <= kWideMaxChunks && ((uintptr_t)content % 8) == 0 && g_tune[13].load(std::memory_order_relaxed) != 0) {
+        // wide form: block sums over the whole GPU, then one chain per chunk
+        ScratchLease scratch(s);  // block sums (64 KiB per chunk) + chunk digests
+        hipError_t e = scratch.get(n * kChunkBlocks * 64 + n * 8);
+        if (e != hipSuccess) return e;
+        uint64_t* S = static_cast<uint64_t*>(scratch.p);
+        uint64_t* h = S + n * kChunkBlocks * 8;
+        hipLaunchKernelGGL(k_manifest_sums, dim3(kChunkBlocks / 16, (unsigned)n), dim3(256), 0, s, content, len, S);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_manifest_chain, dim3((unsigned)n), dim3(256), 0, s, content, len, S, h);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_manifest_fold, dim3(1), dim3(64), 0, s, h, n, out);
+        return hipGetLastError();
+    }
     ScratchLease scratch(s);  // chunk offsets, lengths and digests
     hipError_t e = scratch.get(n * 20);
     if (e != hipSuccess) return e;

@@ -228,7 +228,11 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_DESC_SPLIT           [0] 1 = XXH3 descriptor pages of 4, 8, 12 or
  *                                     16 KiB are hashed in 4 KiB slices dealt
  *                                     to the groups round by round; 0 = one
- *                                     group walks each page (measured faster) */
+ *                                     group walks each page (measured faster)
+ *   PCS_TUNE_MANIFEST_WIDE        [1] manifests of <= 256 chunks at 8-byte
+ *                                     alignment: block sums over the whole GPU
+ *                                     then one chain per chunk (0 = one
+ *                                     workgroup per chunk) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -242,6 +246,7 @@ enum pcs_tune_key {
     PCS_TUNE_DESC_SORT = 10,
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_DESC_SPLIT = 12,
+    PCS_TUNE_MANIFEST_WIDE = 13,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

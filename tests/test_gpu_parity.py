@@ -597,3 +597,29 @@ def test_stamp_while_gpu_busy(use_side_stream):
     for _ in range(3):
         torch.cuda._sleep(3_000_000)
         assert pcs.manifest_checksum_host(content) == oracle.manifest_checksum(content)
+
+
+@pytest.mark.parametrize("wide", [1, 0])
+def test_manifest_forms_vs_oracle(wide):
+    """ManifestBuilder::CalcChecksum (root_meta.cpp:150-174) through both the
+    wide (block sums over the GPU + chain per chunk) and the per-chunk-
+    workgroup forms: last chunks in every XXH3 length class, aligned and
+    unaligned content."""
+    MiB = 1 << 20
+    lens = [1, 16, 17, 128, 129, 240, 241, 2047, 2048, 2049, 100000, MiB - 1, MiB, MiB + 1, MiB + 16, MiB + 200,
+            MiB + 2047, MiB + 2048, 3 * MiB + 777, 7 * MiB]
+    host = np.random.default_rng(17).integers(0, 256, size=7 * MiB + 64, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).to(DEV)
+    d_out = torch.empty(1, dtype=torch.int64, device=DEV)
+    saved = pcs.get_tuning(pcs.TUNE_MANIFEST_WIDE)
+    pcs.set_tuning(pcs.TUNE_MANIFEST_WIDE, wide)
+    try:
+        for shift in (0, 8, 3):  # 16-aligned, 8-aligned, unaligned content
+            for L in lens:
+                want = oracle.manifest_checksum(host[shift:shift + L])
+                pcs._call("pcs_manifest_checksum_dev", dbuf.data_ptr() + shift, L, d_out.data_ptr(),
+                          pcs._stream(None))
+                assert int(u64(d_out)[0]) == want, (wide, shift, L)
+        assert pcs.manifest_checksum_host(host[:3 * MiB + 5].tobytes()) == oracle.manifest_checksum(host[:3 * MiB + 5])
+    finally:
+        pcs.set_tuning(pcs.TUNE_MANIFEST_WIDE, saved)
