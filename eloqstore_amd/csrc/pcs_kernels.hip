@@ -416,68 +416,89 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
 // serial chain (the long-range kernel's scheme, k_xxh3_long).  A slice's last
 // block needs the next slice's first word (its carry); it is left out of the
 // group's sum and added by the chain from the word the next group publishes.
+// One tile of the split scheme: PPB = 16 / G pages, group grp = (page slot ps,
+// slice j).  page_at(ps) gives the page's address (nullptr: no page in that
+// slot).  S holds PPB * P/1024 block-sum records of 4 pairs x 2 u64 (512 u64),
+// C the 16 slice carry words.  On return (after one block barrier) the page
+// digests and verdicts are in tile_h / tile_ok[ps]; the caller must barrier
+// before reading them.
+template <int P, bool NT, typename PageAt>
+__device__ __forceinline__ void xxh3_split_tile(const Xxh3Lane& L, PageAt page_at, uint64_t* S, uint64_t* C,
+                                                uint64_t* tile_h, uint8_t* tile_ok) {
+    static_assert(P % 4096 == 0 && P >= 8192 && P <= 65536, "split pages are 8..64 KiB");
+    constexpr int G = P / 4096;       // groups per page
+    constexpr int NB = P / 1024 - 1;  // full blocks (xxhash.h:5996); block NB is the final one, 4 chunks
+    constexpr int NB1 = NB + 1;
+    const int grp = threadIdx.x >> 4, ps = grp / G, j = grp % G, p = L.g & 3;
+    const uint8_t* page = page_at(ps);
+    uint64_t stored = 0;
+    if (page) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(page + 4096u * j) + L.g;
+        u32x4 d[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[i][c] = ld16<NT>(base + i * 64 + c * 16);
+        stored = lo64(d[0][0]);
+        if (L.g == 0) C[ps * G + j] = lo64(d[0][0]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint64_t Te, To;
+            if (i < 3) xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
+            else if (j < G - 1) xxh3_block_terms<false, true>(L, d[i], 0, 4, Te, To);
+            else xxh3_block_terms<true>(L, d[i], 0, 4, Te, To);
+            if (L.g < 4) {
+                uint64_t* r = S + ((ps * NB1 + 4 * j + i) * 4 + p) * 2;
+                r[0] = Te;
+                r[1] = To;
+            }
+        }
+    }
+    __syncthreads();
+    if (j == 0 && page) {
+        const uint64_t k22 = c_keys.acc[22];  // key of a block's last input word (stripe 15, lane 7)
+        const uint64_t* Sp = S + (ps * NB1 * 4 + p) * 2;
+        uint64_t Ae = L.init_e, Ao = L.init_o;
+#pragma unroll 4
+        for (int b = 0; b < NB; ++b) {
+            uint64_t Te = Sp[b * 8], To = Sp[b * 8 + 1];
+            if ((b & 3) == 3 && p == 3) {  // slice boundary: add the carry word's terms
+                const uint64_t cw = C[ps * G + ((b + 1) >> 2)];
+                Te += cw;
+                To += mul32x32(cw ^ k22);
+            }
+            Ae = xxh3_scramble(Ae + Te, L.ks_e);
+            Ao = xxh3_scramble(Ao + To, L.ks_o);
+        }
+        const uint64_t h = xxh3_merge(L, Ae + Sp[NB * 8], Ao + Sp[NB * 8 + 1], (uint64_t)(P - 8));
+        if (L.g == 0) {
+            tile_h[ps] = h;
+            tile_ok[ps] = (h == stored) ? 1 : 0;
+        }
+    }
+}
+
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                    unsigned long long* first_bad) {
-    static_assert(P % 4096 == 0 && P >= 8192 && P <= 65536, "split pages are 8..64 KiB");
-    constexpr int G = P / 4096;        // groups per page
-    constexpr int PPB = 16 / G;        // pages per 256-thread block
-    constexpr int NB = P / 1024 - 1;   // full blocks (xxhash.h:5996); block NB is the final one, 4 chunks
-    __shared__ uint64_t S[PPB][NB + 1][4][2];  // block sums per accumulator pair (even, odd)
-    __shared__ uint64_t C[PPB][G];             // first input word of each slice (the previous block's carry)
+    constexpr int PPB = 16 / (P / 4096);  // pages per 256-thread block
+    __shared__ uint64_t S[64 * 8];        // block sums per accumulator pair (even, odd)
+    __shared__ uint64_t C[16];            // first input word of each slice (the previous block's carry)
     __shared__ uint64_t tile_h[16];
     __shared__ uint8_t tile_ok[16];
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-    const int grp = threadIdx.x >> 4, ps = grp / G, j = grp % G, p = L.g & 3;
     const uint64_t ntiles = (n + PPB - 1) / PPB;
     const bool remap = gridDim.x == ntiles;
-    const uint64_t k22 = c_keys.acc[22];  // key of a block's last input word (stripe 15, lane 7)
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
         const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        const uint64_t pg = t * PPB + ps;
-        uint64_t stored = 0;
-        if (pg < n) {
-            const u32x4* base = reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P + 4096u * j) + L.g;
-            u32x4 d[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) d[i][c] = ld16<NT>(base + i * 64 + c * 16);
-            stored = lo64(d[0][0]);
-            if (L.g == 0) C[ps][j] = lo64(d[0][0]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                uint64_t Te, To;
-                if (i < 3) xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
-                else if (j < G - 1) xxh3_block_terms<false, true>(L, d[i], 0, 4, Te, To);
-                else xxh3_block_terms<true>(L, d[i], 0, 4, Te, To);
-                if (L.g < 4) {
-                    S[ps][4 * j + i][p][0] = Te;
-                    S[ps][4 * j + i][p][1] = To;
-                }
-            }
-        }
-        __syncthreads();
-        if (j == 0 && pg < n) {
-            uint64_t Ae = L.init_e, Ao = L.init_o;
-#pragma unroll 4
-            for (int b = 0; b < NB; ++b) {
-                uint64_t Te = S[ps][b][p][0], To = S[ps][b][p][1];
-                if ((b & 3) == 3 && p == 3) {  // slice boundary: add the carry word's terms
-                    const uint64_t cw = C[ps][(b + 1) >> 2];
-                    Te += cw;
-                    To += mul32x32(cw ^ k22);
-                }
-                Ae = xxh3_scramble(Ae + Te, L.ks_e);
-                Ao = xxh3_scramble(Ao + To, L.ks_o);
-            }
-            const uint64_t h = xxh3_merge(L, Ae + S[ps][NB][p][0], Ao + S[ps][NB][p][1], (uint64_t)(P - 8));
-            if (L.g == 0) {
-                tile_h[ps] = h;
-                tile_ok[ps] = (h == stored) ? 1 : 0;
-            }
-        }
+        xxh3_split_tile<P, NT>(
+            L,
+            [&](int ps) -> const uint8_t* {
+                const uint64_t pg = t * PPB + ps;
+                return pg < n ? pages + pg * (uint64_t)P : nullptr;
+            },
+            S, C, tile_h, tile_ok);
         __syncthreads();
         const uint64_t i0 = t * PPB;
         if (threadIdx.x < PPB && i0 + threadIdx.x < n) {
@@ -1219,35 +1240,46 @@ __device__ uint64_t xxh64_any(const uint8_t* p, uint64_t len, uint64_t seed) {  
 // stored digest in [0, 8)); SKIP = 0 hashes the raw range.  With FILTER set,
 // ranges the fast kernels handle are skipped.
 template <int MODE>
+__device__ __forceinline__ void generic_one(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                            const uint32_t* __restrict__ len, uint64_t i, int algo, uint64_t seed,
+                                            int skip, uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                            unsigned long long* first_bad) {
+    const uint64_t o = off[i];
+    const uint32_t L = len[i];
+    const uint8_t* p = base + o;
+    if ((uint32_t)skip > L) {  // page shorter than its digest header: never valid
+        if (MODE == kValidate) {
+            ok[i] = 0;
+            if (out) out[i] = 0;
+            if (first_bad) note_bad(first_bad, i);
+        } else if (MODE == kDigest) {
+            out[i] = 0;
+        }
+        return;
+    }
+    const uint64_t h = algo == 0 ? xxh3_any(p + skip, L - skip) : xxh64_any(p + skip, L - skip, seed);
+    const uint64_t stored = skip ? ld64(p) : 0;
+    if (MODE == kStamp) {
+        __builtin_memcpy(const_cast<uint8_t*>(p), &h, 8);
+        if (out) out[i] = h;
+    } else {
+        emit(MODE, i, h, stored, nullptr, out, ok, first_bad);
+    }
+}
+
+// One lane per range.  SKIP = 8 applies the page convention (hash [8, len),
+// stored digest in [0, 8)); SKIP = 0 hashes the raw range.  With FILTER set,
+// ranges the fast kernels handle are skipped.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ len, uint64_t n, int algo,
                                                      uint64_t seed, int skip, int filter, uint64_t* __restrict__ out,
                                                      uint8_t* __restrict__ ok, unsigned long long* first_bad) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t o = off[i];
-        const uint32_t L = len[i];
-        if (filter == 1 && (algo == 0 ? xxh3_fast_ok(o, L) : xxh64_fast_ok(o, L))) continue;
-        if (filter == 2 && xxh3_long_ok(base + o, L)) continue;
-        const uint8_t* p = base + o;
-        if ((uint32_t)skip > L) {  // page shorter than its digest header: never valid
-            if (MODE == kValidate) {
-                ok[i] = 0;
-                if (out) out[i] = 0;
-                if (first_bad) note_bad(first_bad, i);
-            } else if (MODE == kDigest) {
-                out[i] = 0;
-            }
-            continue;
-        }
-        const uint64_t h = algo == 0 ? xxh3_any(p + skip, L - skip) : xxh64_any(p + skip, L - skip, seed);
-        const uint64_t stored = skip ? ld64(p) : 0;
-        if (MODE == kStamp) {
-            __builtin_memcpy(const_cast<uint8_t*>(p), &h, 8);
-            if (out) out[i] = h;
-        } else {
-            emit(MODE, i, h, stored, nullptr, out, ok, first_bad);
-        }
+        if (filter == 1 && (algo == 0 ? xxh3_fast_ok(off[i], len[i]) : xxh64_fast_ok(off[i], len[i]))) continue;
+        if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
+        generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
     }
 }
 
