@@ -655,12 +655,21 @@ enum Addr : int { kAddrStride = 0, kAddrDesc = 1, kAddrList = 2 };
 
 // DEPTH segments are loaded before the first of them is hashed (DEPTH x 4 KiB
 // per wave in flight).
-template <int MODE, bool NT, int ADDR, int DEPTH>
+// SORT (descriptor batches, PCS_TUNE_XXH64_DESC_SORT): the block's 64 pages
+// are handed to its waves in order of size, so a wave no longer walks 16 KiB
+// of segments for mostly shorter pages (~58 % of lane slots useful unsorted,
+// ~85 % sorted on config 3).  Measured 4 % SLOWER on config 3 (6.16 vs 6.42
+// TB/s, profiles/r01/x64_sort_lab.txt): the block is held until its slowest
+// (all-16 KiB) wave ends, so the idle slots move from lanes to whole waves.
+// Off by default; kept as a tested variant.
+template <int MODE, bool NT, int ADDR, int DEPTH, bool SORT = false>
 __global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                   unsigned long long* first_bad) {
     __shared__ __attribute__((aligned(16))) u32x4 lds[4][16][16];  // [wave][page slot][16 B slot]
+    __shared__ uint32_t s_key[SORT ? 64 : 1];
+    __shared__ uint8_t s_perm[SORT ? 64 : 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = lane >> 4, t = lane & 15;        // loader role
     const int i = (lane >> 2) & 3, q = lane & 3;   // hasher role: page 4i + r, quad lane q
@@ -668,14 +677,41 @@ __global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ b
     const uint64_t ntiles = (n + 63) / 64;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t W = (remap ? xcd_tile(t0, ntiles) : t0) * 64 + (uint64_t)wv * 16;
+        const uint64_t T = (remap ? xcd_tile(t0, ntiles) : t0) * 64;
+        if constexpr (SORT) {
+            if (threadIdx.x < 64) {
+                const uint64_t pg = T + threadIdx.x;
+                uint32_t key = 0;  // pages the fast path skips sort first (no segments)
+                if (pg < n) {
+                    const uint32_t L = len[pg];
+                    key = xxh64_lines_ok(off[pg], L) ? L : 0;
+                }
+                s_key[threadIdx.x] = key;
+            }
+            __syncthreads();
+            if (threadIdx.x < 64) {
+                const uint32_t mine = s_key[threadIdx.x];
+                int rank = 0;
+                for (int k = 0; k < 64; ++k) {
+                    const uint32_t other = s_key[k];
+                    rank += (other < mine) || (other == mine && k < (int)threadIdx.x);
+                }
+                s_perm[rank] = (uint8_t)threadIdx.x;
+            }
+            __syncthreads();
+        }
+        // page in wave slot j (0..15) of this wave
+        auto page_at = [&](int j) -> uint64_t {
+            const int slot = wv * 16 + j;
+            return T + (SORT ? s_perm[slot] : slot);
+        };
         // loader pages (4ii + r) and hasher page (4i + r)
         const uint8_t* lp[4];
         uint32_t lP[4];
         uint32_t segs = 0;  // segments this wave must walk (max over its pages)
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
-            const uint64_t pg = W + 4 * ii + r;
+            const uint64_t pg = page_at(4 * ii + r);
             uint32_t P = 0;
             const uint8_t* p = nullptr;
             if (pg < n) {
@@ -694,7 +730,7 @@ __global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ b
             lp[ii] = p;
             lP[ii] = P;
         }
-        const uint64_t hp = W + 4 * i + r;
+        const uint64_t hp = page_at(4 * i + r);
         uint32_t Ph = 0;
         const uint8_t* hptr = nullptr;
 #pragma unroll
@@ -766,6 +802,7 @@ __global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ b
             h = xxh64_avalanche(h);
             if (q == 0) emit(MODE, hp, h, stored, const_cast<uint8_t*>(hptr), out, ok, first_bad);
         }
+        if constexpr (SORT) __syncthreads();  // s_key / s_perm are rewritten by the next tile
     }
 }
 
@@ -1394,7 +1431,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 14;
+constexpr int kTuneKeys = 15;
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1402,7 +1439,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*descriptor tiles sorted by page size*/ 0,
                                           /*zero-copy page list in kernel arguments*/ 1,
                                           /*descriptor pages in 4 KiB slices*/ 0,
-                                          /*manifest: wide block sums + chain kernel*/ 1};
+                                          /*manifest: wide block sums + chain kernel*/ 1,
+                                          /*xxh64 descriptor tiles sorted by page size*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
@@ -1442,10 +1480,19 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
                       uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, unsigned long long* fb) {
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
     const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
-#define L(D) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
-    if (depth == 1) L(1);
-    else if (depth == 2) L(2);
-    else L(4);
+    const bool sort = ADDR == kAddrDesc && g_tune[14].load(std::memory_order_relaxed) != 0;
+#define L(D, S) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, S>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
+    if constexpr (ADDR == kAddrDesc) {
+        if (sort) {
+            if (depth == 1) L(1, true);
+            else if (depth == 2) L(2, true);
+            else L(4, true);
+            return;
+        }
+    }
+    if (depth == 1) L(1, false);
+    else if (depth == 2) L(2, false);
+    else L(4, false);
 #undef L
 }
 

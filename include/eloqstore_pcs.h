@@ -232,7 +232,10 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_MANIFEST_WIDE        [1] manifests of <= 256 chunks at 8-byte
  *                                     alignment: block sums over the whole GPU
  *                                     then one chain per chunk (0 = one
- *                                     workgroup per chunk) */
+ *                                     workgroup per chunk)
+ *   PCS_TUNE_XXH64_DESC_SORT      [0] XXH64 descriptor batches: 1 = hand
+ *                                     each 64-page tile to the four waves in
+ *                                     order of page size (measured slower) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -247,6 +250,7 @@ enum pcs_tune_key {
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_DESC_SPLIT = 12,
     PCS_TUNE_MANIFEST_WIDE = 13,
+    PCS_TUNE_XXH64_DESC_SORT = 14,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -32,12 +32,14 @@ VARIANTS = {
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "desc_sort": {pcs.TUNE_DESC_SORT: 1},
     "desc_split": {pcs.TUNE_DESC_SPLIT: 1},
+    "x64_desc_sort": {pcs.TUNE_XXH64_DESC_SORT: 1},
+    "x64_desc_sort_depth1": {pcs.TUNE_XXH64_DESC_SORT: 1, pcs.TUNE_XXH64_LAYOUT: 2},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = list(range(1, 13))
+    keys = list(range(1, 15))
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -69,7 +71,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_quad",
-                                   "desc_sort", "desc_split"],
+                                   "desc_sort", "desc_split", "x64_desc_sort", "x64_desc_sort_depth1"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):
@@ -83,3 +85,16 @@ def test_variant_mixed_desc(tuned, algo):
     want = np.array([oracle.pages_digest(host[o:o + l], int(l), algo)[0] for o, l in zip(offs, lens)], dtype=np.uint64)
     got = pcs.desc_digest(base, d_off, d_len, n, algo).cpu().numpy().view(np.uint64)
     assert np.array_equal(got, want), (tuned, np.flatnonzero(got != want)[:8])
+    # stamp, validate, corrupt every 7th page from page 3: verdicts and the
+    # first bad index must not depend on the order pages are hashed in
+    pcs.desc_stamp(base, d_off, d_len, n, algo)
+    hdr = base.cpu().numpy()
+    assert np.array_equal(np.array([hdr[o:o + 8].view(np.uint64)[0] for o in offs], dtype=np.uint64), want)
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert ok.cpu().numpy().all()
+    bad = np.arange(3, n, 7)
+    flip = torch.from_numpy((offs[bad] + 10).astype(np.int64)).to(DEV)
+    base[flip] ^= 0x5A
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert np.array_equal(np.flatnonzero(ok.cpu().numpy() == 0), bad), tuned
+    assert int(fb.cpu().numpy().view(np.uint64)[0]) == 3

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--split", default="8192", help="XXH3 split-page thresholds to compare (0 = group per page)")
     ap.add_argument("--sort", default="0", help="descriptor tile sort by size (XXH3 rt batch 1 only)")
     ap.add_argument("--dsplit", default="1", help="XXH3 descriptor pages in 4 KiB slices (1) or not (0)")
+    ap.add_argument("--x64-sort", default="0", help="XXH64 descriptor tiles sorted by size (1) or not (0)")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
     args = ap.parse_args()
     dev = "cuda:0"
@@ -76,12 +77,13 @@ def main():
             key = pcs.TUNE_XXH3_BLOCKS_PER_CU if algo == 0 else pcs.TUNE_XXH64_BLOCKS_PER_CU
             layouts = [int(x) for x in (args.x64_layouts if algo == 1 else args.rt_batch).split(",")]
             splits = [int(x) for x in args.split.split(",")] if algo == 0 else [0]
-            sorts = [(a, b) for a in [int(x) for x in args.sort.split(",")] for b in [int(x) for x in args.dsplit.split(",")]] if algo == 0 else [(0, 1)]
+            sorts = ([(a, b) for a in [int(x) for x in args.sort.split(",")] for b in [int(x) for x in args.dsplit.split(",")]]
+                     if algo == 0 else [(a, 1) for a in [int(x) for x in args.x64_sort.split(",")]])
             for lay in layouts:
                 for sp in [(a, b) for a in splits for b in sorts]:
                     for bpc in bpcs:
                         for nt in nts:
-                            tag = (f" lay={lay}" if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
+                            tag = (f" lay={lay}" + (" sort" if sp[1][0] else "") if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
                                    + (" sort" if sp[1][0] else "") + ("" if sp[1][1] else " nodsplit"))
                             variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
                                              (lay, sp)))
@@ -93,7 +95,8 @@ def main():
             _, algo, key, bpc, nt, kind, (lay, (sp, (srt, dsp))) = v
             pcs.set_tuning(key, bpc)
             pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, sp if sp >= 0 else 0)
-            pcs.set_tuning(pcs.TUNE_DESC_SORT, srt)
+            pcs.set_tuning(pcs.TUNE_DESC_SORT, srt if algo == 0 else 0)
+            pcs.set_tuning(pcs.TUNE_XXH64_DESC_SORT, srt if algo == 1 else 0)
             pcs.set_tuning(pcs.TUNE_DESC_SPLIT, dsp)
             if algo == 1:
                 pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
