@@ -161,15 +161,21 @@ class Workload:
         return self.bytes + (1 if mode == "validate" else 8) * self.n
 
     def read_ceiling(self, reps: int) -> float | None:
-        if self.P is None or self.P not in (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
-            return None
         scratch = torch.empty_like(self.out)  # keep self.out = the digests of the timed steps
-        pcs.read_ceiling(self.pages, self.P, self.n, scratch)
+        if self.P is None:  # mixed sizes: the descriptor kernel's load pattern
+            def run():
+                pcs.read_ceiling_desc(self.pages, self.d_off, self.d_len, self.n, scratch)
+        elif self.P in (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
+            def run():
+                pcs.read_ceiling(self.pages, self.P, self.n, scratch)
+        else:
+            return None
+        run()
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         for _ in range(reps):
-            pcs.read_ceiling(self.pages, self.P, self.n, scratch)
+            run()
         ev[1].record()
         torch.cuda.synchronize()
         t = ev[0].elapsed_time(ev[1]) / 1e3 / reps

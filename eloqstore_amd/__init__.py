@@ -59,6 +59,7 @@ _SIGS = {
     "pcs_gen_desc_dev": [_vp, _vp, _vp, _u64, _u64, _u64, _vp],
     "pcs_flip_byte_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
     "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
+    "pcs_read_ceiling_desc_dev": [_vp, _vp, _vp, _u64, _vp, _vp],
     "pcs_host_alloc_pinned": [_u64, _P(_vp)],
     "pcs_host_free_pinned": [_vp],
     "pcs_host_register": [_vp, _u64],
@@ -260,6 +261,10 @@ def flip_byte(pages, page_size: int, n: int, every: int, byte_offset: int = 10, 
 
 def read_ceiling(pages, page_size: int, n: int, out, stream=None) -> None:
     _call("pcs_read_ceiling_dev", _ptr(pages), page_size, n, _ptr(out), _stream(stream))
+
+
+def read_ceiling_desc(base, off, length, n: int, out, stream=None) -> None:
+    _call("pcs_read_ceiling_desc_dev", _ptr(base), _ptr(off), _ptr(length), n, _ptr(out), _stream(stream))
 
 
 def manifest_checksum_host(content: bytes) -> int:

@@ -882,4 +882,13 @@ int pcs_read_ceiling_dev(const void* d_pages, uint64_t page_size, uint64_t n_pag
     return finish(e, "read-ceiling kernel launch");
 }
 
+int pcs_read_ceiling_desc_dev(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n,
+                              uint64_t* d_out, pcs_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (n && (!d_base || !d_off || !d_len || !d_out)) return fail(PCS_ERR_INVALID, "null pointer");
+    return finish(pcs::run_read_ceiling_desc(static_cast<const uint8_t*>(d_base), d_off, d_len, n, d_out,
+                                             reinterpret_cast<hipStream_t>(stream)),
+                  "read-ceiling kernel launch");
+}
+
 }  // extern "C"

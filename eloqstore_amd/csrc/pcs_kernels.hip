@@ -1244,7 +1244,14 @@ __global__ void k_flip_byte(uint8_t* pages, uint64_t P, uint64_t n, uint64_t eve
     if (p < n) pages[p * P + byte_off] ^= 0xFF;
 }
 
-// Second pass of a two-pass stamp: page i bytes [0, 8) = digest[i].
+// Second pass of a two-pass stamp: page i bytes [0, 8) = digest[i], one
+// non-temporal store per page.  A plain store makes this kernel faster (33 vs
+// 55 us for 1 M headers) but leaves the lines dirty in cache, and their
+// write-back then lands inside the next launch: back-to-back stamps took 711
+// us each with plain stores against 644 us with nt.  Whole 64-byte header
+// lines from a compact copy (pass 1 keeping the page's first line) cost more
+// in pass 1 than they save here (725-745 us per stamp;
+// tools/lab/stamp_line_lab.hip, profiles/r01/stamp_line_lab.txt).
 __global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pages, uint64_t P, uint64_t n,
                                                       const uint64_t* __restrict__ dig) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1255,6 +1262,56 @@ __global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pag
 // (or, SPLIT, as k_xxh3_split<P, kDigest>: G = P / 4096 groups per page, one
 // 4 KiB slice each) with the hash replaced by an xor/add fold: the achievable
 // rate of the product's layout (the roofline's "measured ceiling").
+// Read ceiling for descriptor batches: page pg (off[pg], len[pg] with
+// len % 256 == 0, 16-byte aligned; others are skipped) read by one 16-lane
+// group like xxh3_page_rt4 — 16 nt loads of 16 B per lane per 4 KiB step —
+// folded with xor/add, one 8-byte result per page staged per tile.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_read_ceiling_desc(const uint8_t* __restrict__ base,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ len, uint64_t n,
+                                                          uint64_t* __restrict__ out) {
+    __shared__ uint64_t tile_r[16];
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint64_t ntiles = (n + 15) / 16;
+    const bool remap = gridDim.x == ntiles;
+    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
+        const uint64_t pg = t * 16 + grp;
+        uint64_t r = 0;
+        if (pg < n) {
+            const uint64_t o = off[pg];
+            const uint32_t P = len[pg];
+            if (xxh3_fast_ok(o, P)) {
+                const u32x4* p = reinterpret_cast<const u32x4*>(base + o) + g;
+                const uint32_t steps = P / 4096, rest = (P % 4096) / 256;
+                uint32_t x = 0, y = 0, z = 0, w = 0;
+                for (uint32_t k = 0; k < steps; ++k) {
+                    u32x4 d[16];
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) d[c] = ld16<NT>(p + (k * 16 + c) * 16);
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) { x ^= d[c].x; y += d[c].y; z ^= d[c].z; w += d[c].w; }
+                }
+                for (uint32_t c = 0; c < rest; ++c) {
+                    const u32x4 v = ld16<NT>(p + (steps * 16 + c) * 16);
+                    x ^= v.x; y += v.y; z ^= v.z; w += v.w;
+                }
+                r = ((uint64_t)(x ^ z) << 32) | (y + w);
+            }
+        }
+        r ^= dpp64<kRowRor1>(r);
+        r ^= dpp64<kRowRor2>(r);
+        r ^= dpp64<kRowRor4>(r);
+        r ^= dpp64<kRowRor8>(r);
+        if (g == 0) tile_r[grp] = r;
+        __syncthreads();
+        const uint64_t i = t * 16 + threadIdx.x;
+        if (threadIdx.x < 16 && i < n) st_nt(out + i, tile_r[threadIdx.x]);
+        __syncthreads();
+    }
+}
+
 template <int P, bool NT, bool SPLIT>
 __global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
                                                      uint64_t* __restrict__ out) {
@@ -1796,6 +1853,18 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
     const uint64_t count = (n + every - 1) / every;
     const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_flip_byte, dim3(grid), dim3(kBlock), 0, s, pages, P, n, every, byte_off);
+    return hipGetLastError();
+}
+
+// Descriptor batches (config 3): k_read_ceiling_desc mirrors k_xxh3_desc's
+// loads — one group per page, 16 pages per block, 4 KiB (16 loads per lane)
+// per step, 256 B steps for the rest — with the hash removed.
+hipError_t run_read_ceiling_desc(const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
+                                 uint64_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = page_grid(n, kBlock / 16, 1);
+    if (use_nt()) hipLaunchKernelGGL((k_read_ceiling_desc<true>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out);
+    else hipLaunchKernelGGL((k_read_ceiling_desc<false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out);
     return hipGetLastError();
 }
 

@@ -279,6 +279,11 @@ int pcs_flip_byte_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, uint6
  * split slices for the page sizes PCS_TUNE_XXH3_SPLIT_PAGES selects). */
 int pcs_read_ceiling_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages,
                          uint64_t *d_out, pcs_stream_t stream);
+/* The same for descriptor batches: the XXH3 descriptor kernel's loads (one
+ * 16-lane group per page, 4 KiB per step) over pages with len % 256 == 0 at
+ * 16-byte-aligned offsets (others are skipped, their result is 0). */
+int pcs_read_ceiling_desc_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                              uint64_t n, uint64_t *d_out, pcs_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -414,6 +414,27 @@ def test_read_ceiling_fold(P):
     assert np.array_equal(u64(out), _ceiling_fold(buf.cpu().numpy(), P))
 
 
+def test_read_ceiling_desc_fold():
+    """The config-3 read ceiling (descriptor layout) reads every byte of every
+    page: one 16-lane group per page, no slices."""
+    n = 700
+    offs, lens, total = mixed_layout(0x5EED0003, 0, n)
+    base = torch.empty(total, dtype=torch.uint8, device=DEV)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+    pcs.gen_desc(base, d_off, d_len, n, 0x5EED0003, 0)
+    out = torch.empty(n, dtype=torch.int64, device=DEV)
+    pcs.read_ceiling_desc(base, d_off, d_len, n, out)
+    host = base.cpu().numpy()
+    saved = pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES)
+    pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, 0)  # the fold helper then folds whole pages
+    try:
+        want = np.array([_ceiling_fold(host[o:o + l], int(l))[0] for o, l in zip(offs, lens)], dtype=np.uint64)
+    finally:
+        pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, saved)
+    assert np.array_equal(u64(out), want)
+
+
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_host_direct_pinned_path(algo):
     """Contiguous pinned pages take the direct-DMA branch of the host pipeline

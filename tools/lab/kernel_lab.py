@@ -24,6 +24,19 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import eloqstore_amd as pcs  # noqa: E402
 from workload import mixed_layout  # noqa: E402
 
+if "--lib" in sys.argv:  # A/B against another build of the library (e.g. an older commit)
+    _path = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+    _probe = ctypes.CDLL(_path)
+    pcs.LIB_PATH = _path
+    pcs._SIGS = {k: v for k, v in pcs._SIGS.items() if hasattr(_probe, k)}
+
+
+def set_tuning_if_known(key, value):
+    try:
+        pcs.set_tuning(key, value)
+    except pcs.PcsError:
+        pass  # an older library without this knob
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -37,8 +50,10 @@ def main():
     ap.add_argument("--rt-batch", default="1", help="XXH3 run-time-size kernels: 1 = 4-block batches, 0 = one block")
     ap.add_argument("--split", default="8192", help="XXH3 split-page thresholds to compare (0 = group per page)")
     ap.add_argument("--sort", default="0", help="descriptor tile sort by size (XXH3 rt batch 1 only)")
-    ap.add_argument("--dsplit", default="1", help="XXH3 descriptor pages in 4 KiB slices (1) or not (0)")
+    ap.add_argument("--dsplit", default="0", help="XXH3 descriptor pages in 4 KiB slices (1) or not (0, the product default)")
     ap.add_argument("--x64-sort", default="0", help="XXH64 descriptor tiles sorted by size (1) or not (0)")
+    ap.add_argument("--b2b", type=int, default=0, help="time K back-to-back launches per sample (0 = one launch)")
+    ap.add_argument("--lib", default=None, help="library to load instead of eloqstore_amd/libeloqstore_pcs.so")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
     args = ap.parse_args()
     dev = "cuda:0"
@@ -78,16 +93,17 @@ def main():
             layouts = [int(x) for x in (args.x64_layouts if algo == 1 else args.rt_batch).split(",")]
             splits = [int(x) for x in args.split.split(",")] if algo == 0 else [0]
             sorts = ([(a, b) for a in [int(x) for x in args.sort.split(",")] for b in [int(x) for x in args.dsplit.split(",")]]
-                     if algo == 0 else [(a, 1) for a in [int(x) for x in args.x64_sort.split(",")]])
+                     if algo == 0 else [(a, 0) for a in [int(x) for x in args.x64_sort.split(",")]])
             for lay in layouts:
                 for sp in [(a, b) for a in splits for b in sorts]:
                     for bpc in bpcs:
                         for nt in nts:
                             tag = (f" lay={lay}" + (" sort" if sp[1][0] else "") if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
-                                   + (" sort" if sp[1][0] else "") + ("" if sp[1][1] else " nodsplit"))
+                                   + (" sort" if sp[1][0] else "") + (" dsplit" if sp[1][1] else ""))
                             variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
                                              (lay, sp)))
-        if P in (4096, 65536):
+        has_desc_ceiling = "pcs_read_ceiling_desc_dev" in pcs._SIGS
+        if P in (4096, 65536) or (P is None and has_desc_ceiling):
             for nt in nts:
                 variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", (1, (8192, (0, 1)))))
 
@@ -96,7 +112,7 @@ def main():
             pcs.set_tuning(key, bpc)
             pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, sp if sp >= 0 else 0)
             pcs.set_tuning(pcs.TUNE_DESC_SORT, srt if algo == 0 else 0)
-            pcs.set_tuning(pcs.TUNE_XXH64_DESC_SORT, srt if algo == 1 else 0)
+            set_tuning_if_known(pcs.TUNE_XXH64_DESC_SORT, srt if algo == 1 else 0)
             pcs.set_tuning(pcs.TUNE_DESC_SPLIT, dsp)
             if algo == 1:
                 pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
@@ -106,7 +122,9 @@ def main():
                 pcs.set_tuning(pcs.TUNE_XXH64_NT_LOADS, nt)
             else:
                 pcs.set_tuning(pcs.TUNE_NT_LOADS, nt)
-            if kind == "ceil":
+            if kind == "ceil" and P is None:
+                pcs.read_ceiling_desc(pages, d_off, d_len, n, out)
+            elif kind == "ceil":
                 pcs.read_ceiling(pages, P, n, out)
             elif P is None:
                 pcs.desc_digest(pages, d_off, d_len, n, algo, out=out)
@@ -126,6 +144,15 @@ def main():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(args.rounds):
             for v in variants:
+                if args.b2b:  # K launches back to back, like bench.py's timed loop
+                    torch.cuda.synchronize()
+                    ev0.record()
+                    for _k in range(args.b2b):
+                        run(v)
+                    ev1.record()
+                    torch.cuda.synchronize()
+                    times[v[0]].append(ev0.elapsed_time(ev1) / args.b2b)
+                    continue
                 torch.cuda._sleep(1_000_000)  # keep the GPU busy while the launch is enqueued
                 ev0.record()
                 run(v)
