@@ -8,9 +8,10 @@ pages already resident in HBM; value = page bytes hashed by ALL ranks per
 second (GiB/s, 2^30), per-GPU work fixed (weak scaling: every rank owns its
 own disjoint page range, no collective on the data path).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6|7]
 
 Default (N=1) = BASELINE config 2: 1,048,576 x 4 KiB pages (4 GiB) per GPU.
+Configs 6/7 are the north star's 8/16 KiB page-size sweep (4 GiB per GPU).
 Multi-GPU: launched by torch.distributed.run, one process per GPU; gloo is the
 control plane (barrier + max over ranks of the timed region).
 
@@ -53,6 +54,10 @@ CONFIGS = {
     3: (None, 1 << 20, 0x5EED0003, "config3: mixed 4/8/16 KiB pages, 1M pages per GPU, packed + descriptors"),
     4: (65536, 1 << 18, 0x5EED0004, "config4: 64 KiB chunks, 256K chunks device-resident per GPU"),
     5: (4096, 1 << 23, 0x5EED0005, "config5: 4 KiB pages, 8M pages per GPU (64M over 8 GPUs)"),
+    # page-size sweep named in BASELINE.json's north_star (4 / 16 / 64 KiB batches), not numbered
+    # BASELINE configs: 4 GiB per GPU like config 2 (same numbering as tools/lab/kernel_lab.py)
+    6: (8192, 1 << 19, 0x5EED0006, "sweep: 8 KiB pages, 512K-page device-resident batch per GPU"),
+    7: (16384, 1 << 18, 0x5EED0007, "sweep: 16 KiB pages, 256K-page device-resident batch per GPU"),
 }
 
 
@@ -470,6 +475,11 @@ def main():
                 "mode": f"{args.mode} ({'pcs_pages' if w.P else 'pcs_desc'}_{args.mode}_dev)",
                 "parallelism": f"page shards x{world}, no collective",
             },
+            # whole-job rate against the aggregate HBM peak of all ranks (north_star: "fraction of
+            # the aggregate HBM-read roofline"); roofline below is rank 0's dominant kernel
+            "per_gpu_GiBps": round(value / world, 2),
+            "aggregate_roofline": {"GBps": round(value * GIB / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS * world,
+                                   "frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * world), 4)},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
