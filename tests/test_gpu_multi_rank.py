@@ -1,0 +1,90 @@
+"""The N>1 path on a GPU: two ranks, one process each, sharing cuda:0 of the
+one-GPU box (bench.py maps rank -> device modulo the device count; on a full
+node the map is 1:1).
+
+- Each rank hashes its own page shard with the HIP kernel, checks it against
+  the oracle, and the digests gathered over gloo equal the single-process
+  oracle result: sharding by pcs_shard_range loses and duplicates nothing.
+- bench.py launched the way the driver launches it (torch.distributed.run,
+  127.0.0.1 rendezvous) prints one weak-scaling line from rank 0.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_PAGES, P, SEED = 3001, 4096, 0x5EED0005
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def worker(rank: int, world: int, port: int, out_dir: str):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import eloqstore_amd as pcs
+    import oracle
+
+    torch.cuda.set_device(0)
+    b, e = pcs.shard_range(N_PAGES, world, rank)
+    pages = torch.empty((e - b) * P, dtype=torch.uint8, device="cuda:0")
+    pcs.gen_pages(pages, P, e - b, SEED, b)  # global page indices b..e-1
+    dig = pcs.pages_digest(pages, P, e - b).cpu()
+    own_ok = bool(np.array_equal(dig.numpy().view(np.uint64), oracle.pages_digest(pages.cpu().numpy(), P)))
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([e - b]))
+    maxn = int(max(s.item() for s in sizes))
+    buf = torch.zeros(maxn, dtype=torch.int64)
+    buf[: e - b] = dig
+    parts = [torch.zeros(maxn, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    oks = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(oks, torch.tensor([int(own_ok)]))
+    if rank == 0:
+        gathered = torch.cat([parts[r][: int(sizes[r].item())] for r in range(world)])
+        np.save(os.path.join(out_dir, "gathered.npy"), gathered.numpy())
+        with open(os.path.join(out_dir, "oks.txt"), "w") as f:
+            f.write(" ".join(str(int(o.item())) for o in oks))
+    dist.destroy_process_group()
+
+
+def test_two_ranks_gpu_shards_match_oracle(tmp_path):
+    world = 2
+    mp.spawn(worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    import oracle
+    from workload import fill_pages
+
+    assert open(tmp_path / "oks.txt").read().split() == ["1"] * world
+    gathered = np.load(tmp_path / "gathered.npy").view(np.uint64)
+    single = oracle.pages_digest(fill_pages(SEED, 0, N_PAGES, P).reshape(-1), P)
+    assert np.array_equal(gathered, single)
+
+
+def test_bench_two_ranks_torchrun():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--pages-per-gpu", "65536"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 3
+    assert line["config"]["pages_per_gpu"] == 65536
+    assert line["value"] > 0 and line["aggregate_roofline"]["peak_GBps"] == 2 * 8000.0
+    assert line["corruption_drill"]["pass"]
