@@ -371,15 +371,11 @@ template <int MODE, bool NT, bool B4, bool SORT>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad, int skip_split,
-                                                  const uint32_t* __restrict__ perm) {
-    // perm (PCS_TUNE_DESC_BIN): list position -> page index, pages grouped by
-    // size (k_bin_scatter), so the groups of a wave and the waves of a block
-    // walk pages of one size.  Results are still written by page index.
+                                                  unsigned long long* first_bad, int skip_split) {
     // SORT: the 16 pages of a tile are handed to the groups in order of size,
     // so the four groups of a wave mostly share one size and none idles while
     // a neighbour walks a longer page (mixed-size batches, config 3).
-    __shared__ uint8_t tperm[16];
+    __shared__ uint8_t perm[16];
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
@@ -396,13 +392,12 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                     const uint32_t other = ik < n ? len[ik] : 0xFFFFFFFFu;
                     rank += (other < mine) || (other == mine && k < (int)threadIdx.x);
                 }
-                tperm[rank] = (uint8_t)threadIdx.x;
+                perm[rank] = (uint8_t)threadIdx.x;
             }
             __syncthreads();
-            slot = tperm[threadIdx.x >> 4];
+            slot = perm[threadIdx.x >> 4];
         }
-        const uint64_t li = t * 16 + slot;
-        const uint64_t pg = perm ? (li < n ? perm[li] : n) : li;
+        const uint64_t pg = t * 16 + slot;
         if (pg < n) {
             const uint64_t o = off[pg];
             const uint32_t P = len[pg];
@@ -413,7 +408,7 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                 if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
             }
         }
-        if constexpr (SORT) __syncthreads();  // tperm is rewritten by the next tile
+        if constexpr (SORT) __syncthreads();  // perm is rewritten by the next tile
     }
 }
 
@@ -671,7 +666,7 @@ template <int MODE, bool NT, int ADDR, int DEPTH, bool SORT = false>
 __global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad, const uint32_t* __restrict__ perm) {
+                                                  unsigned long long* first_bad) {
     __shared__ __attribute__((aligned(16))) u32x4 lds[4][16][16];  // [wave][page slot][16 B slot]
     __shared__ uint32_t s_key[SORT ? 64 : 1];
     __shared__ uint8_t s_perm[SORT ? 64 : 1];
@@ -705,12 +700,10 @@ __global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ b
             }
             __syncthreads();
         }
-        // page in wave slot j (0..15) of this wave; perm (PCS_TUNE_DESC_BIN,
-        // descriptor batches) maps list positions to page indices by size
+        // page in wave slot j (0..15) of this wave
         auto page_at = [&](int j) -> uint64_t {
             const int slot = wv * 16 + j;
-            const uint64_t li = T + (SORT ? s_perm[slot] : slot);
-            return perm ? (li < n ? perm[li] : n) : li;
+            return T + (SORT ? s_perm[slot] : slot);
         };
         // loader pages (4ii + r) and hasher page (4i + r)
         const uint8_t* lp[4];
@@ -1495,7 +1488,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 16;
+constexpr int kTuneKeys = 15;
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1504,8 +1497,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*zero-copy page list in kernel arguments*/ 1,
                                           /*descriptor pages in 4 KiB slices*/ 0,
                                           /*manifest: wide block sums + chain kernel*/ 1,
-                                          /*xxh64 descriptor tiles sorted by page size*/ 0,
-                                          /*descriptor batches binned by page size first*/ 0};
+                                          /*xxh64 descriptor tiles sorted by page size*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
@@ -1542,12 +1534,11 @@ bool xxh64_lds_layout() { return g_tune[6].load(std::memory_order_relaxed) != 1;
 // (0 = default depth, 2/3/4 = depth 1/2/4; 1 is the quad layout, not here).
 template <int MODE, bool NT, int ADDR>
 void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                      uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, unsigned long long* fb,
-                      const uint32_t* perm = nullptr) {
+                      uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, unsigned long long* fb) {
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
     const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
     const bool sort = ADDR == kAddrDesc && g_tune[14].load(std::memory_order_relaxed) != 0;
-#define L(D, S) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, S>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb, perm)
+#define L(D, S) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, S>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
     if constexpr (ADDR == kAddrDesc) {
         if (sort) {
             if (depth == 1) L(1, true);
@@ -1683,112 +1674,6 @@ hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t P, uint6
 hipError_t scratch_acquire(size_t bytes, void** out, int* id) { return g_scratch.acquire(bytes, out, id); }
 hipError_t scratch_release(int id, hipStream_t s) { return g_scratch.release(id, s); }
 
-// ---------------------------------------------------------------------------
-// size bins for descriptor batches (PCS_TUNE_DESC_BIN)
-// ---------------------------------------------------------------------------
-// A wave of the descriptor kernels walks the segments of its longest page, and
-// a block stays resident until its longest wave ends.  In a mixed 4/8/16 KiB
-// batch (config 3) that leaves a large share of lane slots idle.  Binning the
-// batch by page size first (a counting sort of page indices, two small
-// kernels) hands every wave and block pages of one size.  bin 0 = pages the
-// fast kernel skips; bin b > 0 = pages of (b-1)*4 KiB < len <= b*4 KiB.
-constexpr int kBins = 32;
-template <int ALGO>
-__device__ __forceinline__ int size_bin(uint64_t o, uint32_t L) {
-    const bool fast = ALGO == 0 ? xxh3_fast_ok(o, L) : xxh64_lines_ok(o, L);
-    return fast ? (int)min<uint32_t>((L + 4095u) / 4096u, (uint32_t)kBins - 1) : 0;
-}
-
-// Block k of the grid owns pages [k*span, (k+1)*span).  k_bin_count writes
-// its per-bin counts to hist[bin][k] (no atomics: one word per block per bin);
-// k_bin_scan turns hist into exclusive offsets over (bin, block) in place, so
-// bin b's pages come first and, inside a bin, block k's pages follow block
-// k-1's; k_bin_scatter writes perm[offset + rank-in-block].  Device-scope
-// atomics on shared counters were measured slower (one word takes ~88 updates
-// per us, MI355X_MICROARCH.md "dequeue").
-template <int ALGO>
-__global__ __launch_bounds__(256) void k_bin_count(const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-                                                  uint64_t n, uint64_t span, unsigned long long* __restrict__ hist) {
-    __shared__ unsigned int h[kBins];
-    if (threadIdx.x < kBins) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t lo = blockIdx.x * span, hi = min(n, lo + span);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) atomicAdd(&h[size_bin<ALGO>(off[i], len[i])], 1u);
-    __syncthreads();
-    if (threadIdx.x < kBins) hist[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
-}
-
-// One workgroup: exclusive scan of hist[kBins * nblk] (bin-major) in place.
-__global__ __launch_bounds__(256) void k_bin_scan(unsigned long long* __restrict__ hist, uint64_t total) {
-    __shared__ unsigned long long part[256];
-    const uint64_t per = (total + 255) / 256, lo = threadIdx.x * per, hi = min(total, lo + per);
-    unsigned long long sum = 0;
-    for (uint64_t i = lo; i < hi; ++i) sum += hist[i];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long acc = 0;
-        for (int k = 0; k < 256; ++k) {
-            const unsigned long long v = part[k];
-            part[k] = acc;
-            acc += v;
-        }
-    }
-    __syncthreads();
-    unsigned long long acc = part[threadIdx.x];
-    for (uint64_t i = lo; i < hi; ++i) {
-        const unsigned long long v = hist[i];
-        hist[i] = acc;
-        acc += v;
-    }
-}
-
-template <int ALGO>
-__global__ __launch_bounds__(256) void k_bin_scatter(const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-                                                    uint64_t n, uint64_t span, const unsigned long long* __restrict__ offs,
-                                                    uint32_t* __restrict__ perm) {
-    __shared__ unsigned int h[kBins];
-    __shared__ unsigned long long base[kBins];
-    if (threadIdx.x < kBins) base[threadIdx.x] = offs[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
-    const uint64_t lo = blockIdx.x * span, hi = min(n, lo + span);
-    for (uint64_t c0 = lo; c0 < hi; c0 += 256) {  // trip count uniform across the block
-        if (threadIdx.x < kBins) h[threadIdx.x] = 0;
-        __syncthreads();
-        const uint64_t i = c0 + threadIdx.x;
-        int b = -1;
-        unsigned int r = 0;
-        if (i < hi) {
-            b = size_bin<ALGO>(off[i], len[i]);
-            r = atomicAdd(&h[b], 1u);
-        }
-        __syncthreads();
-        if (b >= 0) perm[base[b] + r] = (uint32_t)i;
-        __syncthreads();
-        if (threadIdx.x < kBins) base[threadIdx.x] += h[threadIdx.x];
-    }
-}
-
-// Device-side page permutation by size for a descriptor batch, in lease's
-// scratch; nullptr when binning is off or the batch is too small to gain.
-const uint32_t* bin_by_size(int algo, const uint64_t* off, const uint32_t* len, uint64_t n, ScratchLease& lease,
-                            hipStream_t s, hipError_t& e) {
-    e = hipSuccess;
-    if (g_tune[15].load(std::memory_order_relaxed) == 0 || n < 4096 || n > 0xFFFFFFFFull) return nullptr;
-    const unsigned nblk = grid_for(n, 1024, 4);  // >= 1024 pages per block
-    const uint64_t span = (n + nblk - 1) / nblk;
-    const uint64_t hist_words = (uint64_t)kBins * nblk;
-    if ((e = lease.get(hist_words * sizeof(unsigned long long) + n * sizeof(uint32_t))) != hipSuccess) return nullptr;
-    auto* hist = static_cast<unsigned long long*>(lease.p);
-    auto* perm = reinterpret_cast<uint32_t*>(hist + hist_words);
-    if (algo == 0) hipLaunchKernelGGL(k_bin_count<0>, dim3(nblk), dim3(kBlock), 0, s, off, len, n, span, hist);
-    else hipLaunchKernelGGL(k_bin_count<1>, dim3(nblk), dim3(kBlock), 0, s, off, len, n, span, hist);
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(kBlock), 0, s, hist, hist_words);
-    if (algo == 0) hipLaunchKernelGGL(k_bin_scatter<0>, dim3(nblk), dim3(kBlock), 0, s, off, len, n, span, hist, perm);
-    else hipLaunchKernelGGL(k_bin_scatter<1>, dim3(nblk), dim3(kBlock), 0, s, off, len, n, span, hist, perm);
-    if ((e = hipGetLastError()) != hipSuccess) return nullptr;
-    return perm;
-}
-
 template <int MODE>
 static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
                             int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* fb,
@@ -1796,13 +1681,9 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
     if (n == 0) return hipSuccess;
     if (skip == 8 && seed == 0) {
         // fast kernels for conforming pages, generic lanes for the rest
-        ScratchLease bins(s);
-        const int dsplit = algo == 0 && g_tune[12].load(std::memory_order_relaxed) != 0 ? 1 : 0;
-        hipError_t be = hipSuccess;
-        const uint32_t* perm = dsplit ? nullptr : bin_by_size(algo, off, len, n, bins, s, be);
-        if (be != hipSuccess) return be;
         if (algo == 0) {
             const unsigned grid = page_grid(n, kBlock / 16, 1);
+            const int dsplit = g_tune[12].load(std::memory_order_relaxed) != 0 ? 1 : 0;
             if (dsplit) {
                 const unsigned sgrid = (unsigned)std::min<uint64_t>((n + 15) / 16, 0x7FFFFFFFull);
                 if (use_nt())
@@ -1814,7 +1695,7 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             }
 #define L(NT_, B4_, SORT_)                                                                                          \
     hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_, SORT_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, \
-                       fb, dsplit, perm)
+                       fb, dsplit)
             const bool srt = g_tune[10].load(std::memory_order_relaxed) != 0;
             if (use_nt()) {
                 if (rt_batch4()) {
@@ -1831,8 +1712,8 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
             if (xxh64_lds_layout()) {
-                if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, perm);
-                else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, perm);
+                if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
+                else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
                 // pages off the lines shape are left to the quad kernel below
             }
             if (use_nt64())
@@ -1942,7 +1823,7 @@ hipError_t run_list(int mode, int algo, const uint64_t* ptrs, const uint64_t* ho
         // deepest pipeline: over PCIe every segment is a round trip
 #define LAUNCH(M)                                                                                              \
     hipLaunchKernelGGL((k_xxh64_lds<M, false, kAddrList, 4>), dim3(grid), dim3(kBlock), 0, s, nullptr, ptrs, nullptr, \
-                       (uint32_t)P, n, out, ok, nullptr, nullptr)
+                       (uint32_t)P, n, out, ok, nullptr)
         if (mode == kDigest) LAUNCH(kDigest);
         else if (mode == kValidate) LAUNCH(kValidate);
         else LAUNCH(kStamp);

@@ -235,11 +235,7 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     workgroup per chunk)
  *   PCS_TUNE_XXH64_DESC_SORT      [0] XXH64 descriptor batches: 1 = hand
  *                                     each 64-page tile to the four waves in
- *                                     order of page size (measured slower)
- *   PCS_TUNE_DESC_BIN             [0] descriptor batches of >= 4096 pages:
- *                                     1 = counting-sort the page indices by
- *                                     size (4 KiB bins) on the device first,
- *                                     so every wave walks pages of one size */
+ *                                     order of page size (measured slower) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -255,7 +251,6 @@ enum pcs_tune_key {
     PCS_TUNE_DESC_SPLIT = 12,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_DESC_SORT = 14,
-    PCS_TUNE_DESC_BIN = 15,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

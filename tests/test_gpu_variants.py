@@ -34,14 +34,12 @@ VARIANTS = {
     "desc_split": {pcs.TUNE_DESC_SPLIT: 1},
     "x64_desc_sort": {pcs.TUNE_XXH64_DESC_SORT: 1},
     "x64_desc_sort_depth1": {pcs.TUNE_XXH64_DESC_SORT: 1, pcs.TUNE_XXH64_LAYOUT: 2},
-    "desc_bin": {pcs.TUNE_DESC_BIN: 1},
-    "desc_bin_x64_depth1": {pcs.TUNE_DESC_BIN: 1, pcs.TUNE_XXH64_LAYOUT: 2},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = list(range(1, 16))
+    keys = list(range(1, 15))
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -73,12 +71,11 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_quad",
-                                   "desc_sort", "desc_split", "x64_desc_sort", "x64_desc_sort_depth1", "desc_bin",
-                                   "desc_bin_x64_depth1"],
+                                   "desc_sort", "desc_split", "x64_desc_sort", "x64_desc_sort_depth1"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):
-    n = 5000  # >= 4096: size binning (desc_bin) applies
+    n = 2000
     offs, lens, total = mixed_layout(0x5EED0003, 0, n)
     base = torch.empty(total, dtype=torch.uint8, device=DEV)
     d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)

@@ -52,7 +52,6 @@ def main():
     ap.add_argument("--sort", default="0", help="descriptor tile sort by size (XXH3 rt batch 1 only)")
     ap.add_argument("--dsplit", default="0", help="XXH3 descriptor pages in 4 KiB slices (1) or not (0, the product default)")
     ap.add_argument("--x64-sort", default="0", help="XXH64 descriptor tiles sorted by size (1) or not (0)")
-    ap.add_argument("--bin", default="0", help="descriptor batches binned by size first (PCS_TUNE_DESC_BIN)")
     ap.add_argument("--b2b", type=int, default=0, help="time K back-to-back launches per sample (0 = one launch)")
     ap.add_argument("--lib", default=None, help="library to load instead of eloqstore_amd/libeloqstore_pcs.so")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
@@ -99,20 +98,17 @@ def main():
                 for sp in [(a, b) for a in splits for b in sorts]:
                     for bpc in bpcs:
                         for nt in nts:
-                          for binv in [int(x) for x in args.bin.split(",")]:
                             tag = (f" lay={lay}" + (" sort" if sp[1][0] else "") if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
                                    + (" sort" if sp[1][0] else "") + (" dsplit" if sp[1][1] else ""))
-                            tag += " bin" if binv else ""
                             variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
-                                             (lay, sp), binv))
+                                             (lay, sp)))
         has_desc_ceiling = "pcs_read_ceiling_desc_dev" in pcs._SIGS
         if P in (4096, 65536) or (P is None and has_desc_ceiling):
             for nt in nts:
-                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", (1, (8192, (0, 0))), 0))
+                variants.append((f"read-ceiling bpc=0 nt={nt}", 0, pcs.TUNE_XXH3_BLOCKS_PER_CU, 0, nt, "ceil", (1, (8192, (0, 1)))))
 
         def run(v):
-            _, algo, key, bpc, nt, kind, (lay, (sp, (srt, dsp))), binv = v
-            set_tuning_if_known(pcs.TUNE_DESC_BIN, binv)
+            _, algo, key, bpc, nt, kind, (lay, (sp, (srt, dsp))) = v
             pcs.set_tuning(key, bpc)
             pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, sp if sp >= 0 else 0)
             pcs.set_tuning(pcs.TUNE_DESC_SORT, srt if algo == 0 else 0)
