@@ -662,22 +662,26 @@ enum Addr : int { kAddrStride = 0, kAddrDesc = 1, kAddrList = 2 };
 // TB/s, profiles/r01/x64_sort_lab.txt): the block is held until its slowest
 // (all-16 KiB) wave ends, so the idle slots move from lanes to whole waves.
 // Off by default; kept as a tested variant.
-template <int MODE, bool NT, int ADDR, int DEPTH, bool SORT = false>
-__global__ __launch_bounds__(256) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
-                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad) {
-    __shared__ __attribute__((aligned(16))) u32x4 lds[4][16][16];  // [wave][page slot][16 B slot]
+// WPB waves per workgroup (PCS_TUNE_XXH64_WAVES): a workgroup owns 16 * WPB
+// consecutive pages.
+template <int MODE, bool NT, int ADDR, int DEPTH, bool SORT = false, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
+                                                       uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                       unsigned long long* first_bad) {
+    static_assert(!SORT || WPB == 4, "the tile sort ranks 64 pages with the block's first wave");
+    __shared__ __attribute__((aligned(16))) u32x4 lds[WPB][16][16];  // [wave][page slot][16 B slot]
     __shared__ uint32_t s_key[SORT ? 64 : 1];
     __shared__ uint8_t s_perm[SORT ? 64 : 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = lane >> 4, t = lane & 15;        // loader role
     const int i = (lane >> 2) & 3, q = lane & 3;   // hasher role: page 4i + r, quad lane q
     const int a = q == 2 ? 3 : q == 3 ? 2 : q;
-    const uint64_t ntiles = (n + 63) / 64;
+    constexpr uint64_t kTile = 16 * WPB;
+    const uint64_t ntiles = (n + kTile - 1) / kTile;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t T = (remap ? xcd_tile(t0, ntiles) : t0) * 64;
+        const uint64_t T = (remap ? xcd_tile(t0, ntiles) : t0) * kTile;
         if constexpr (SORT) {
             if (threadIdx.x < 64) {
                 const uint64_t pg = T + threadIdx.x;
@@ -1488,7 +1492,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 15;
+constexpr int kTuneKeys = 16;
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1497,7 +1501,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*zero-copy page list in kernel arguments*/ 1,
                                           /*descriptor pages in 4 KiB slices*/ 0,
                                           /*manifest: wide block sums + chain kernel*/ 1,
-                                          /*xxh64 descriptor tiles sorted by page size*/ 0};
+                                          /*xxh64 descriptor tiles sorted by page size*/ 0,
+                                          /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
@@ -1538,6 +1543,23 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
     const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
     const bool sort = ADDR == kAddrDesc && g_tune[14].load(std::memory_order_relaxed) != 0;
+    const int64_t wpb = g_tune[15].load(std::memory_order_relaxed);
+    if (!sort && (wpb == 1 || wpb == 2)) {
+        // one workgroup per 16 * wpb pages, every tile covered once
+        const unsigned g = (unsigned)std::min<uint64_t>((n + 16 * wpb - 1) / (16 * wpb), 0x7FFFFFFFull);
+#define LW(D, W) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, false, W>), dim3(g), dim3(64 * W), 0, s, base, off, len, P, n, out, ok, fb)
+        if (wpb == 1) {
+            if (depth == 1) LW(1, 1);
+            else if (depth == 2) LW(2, 1);
+            else LW(4, 1);
+        } else {
+            if (depth == 1) LW(1, 2);
+            else if (depth == 2) LW(2, 2);
+            else LW(4, 2);
+        }
+#undef LW
+        return;
+    }
 #define L(D, S) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, S>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
     if constexpr (ADDR == kAddrDesc) {
         if (sort) {
@@ -1625,8 +1647,12 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
         const unsigned grid = page_grid(n, kBlock / 4, 2, P);
         const bool lines = aligned16 && P % 64 == 0 && P >= 128;
         if (lines && xxh64_lds_layout()) {
-            if (use_nt()) launch_xxh64_lds<MODE, true, kAddrStride>(grid, s, pages, nullptr, nullptr, (uint32_t)P, n, out, ok, fb);
-            else launch_xxh64_lds<MODE, false, kAddrStride>(grid, s, pages, nullptr, nullptr, (uint32_t)P, n, out, ok, fb);
+            // one workgroup per 64 pages at every page size: the large-page
+            // cap of page_grid (8 per CU) cost the LDS kernel 7-8 % on 64 KiB
+            // pages (profiles/r01/x64_depth_lab.txt, x64_waves_lab.txt)
+            const unsigned lgrid = page_grid(n, kBlock / 4, 2);
+            if (use_nt()) launch_xxh64_lds<MODE, true, kAddrStride>(lgrid, s, pages, nullptr, nullptr, (uint32_t)P, n, out, ok, fb);
+            else launch_xxh64_lds<MODE, false, kAddrStride>(lgrid, s, pages, nullptr, nullptr, (uint32_t)P, n, out, ok, fb);
             return hipGetLastError();
         }
         if (lines && use_nt64())

@@ -235,7 +235,9 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     workgroup per chunk)
  *   PCS_TUNE_XXH64_DESC_SORT      [0] XXH64 descriptor batches: 1 = hand
  *                                     each 64-page tile to the four waves in
- *                                     order of page size (measured slower) */
+ *                                     order of page size (measured slower)
+ *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
+ *                                     kernel (1, 2 or 4; 16 pages per wave) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -251,6 +253,7 @@ enum pcs_tune_key {
     PCS_TUNE_DESC_SPLIT = 12,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_DESC_SORT = 14,
+    PCS_TUNE_XXH64_WAVES = 15,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
