@@ -155,7 +155,6 @@ TUNE_DESC_SPLIT = 12
 TUNE_MANIFEST_WIDE = 13
 TUNE_XXH64_DESC_SORT = 14
 TUNE_XXH64_WAVES = 15
-TUNE_XXH64_DYN = 16
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -811,170 +811,6 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
 }
 
 
-// XXH64 over descriptor pages, slots scheduled per wave (PCS_TUNE_XXH64_DYN).
-//
-// k_xxh64_lds walks every wave to its longest page, so in a mixed 4/8/16 KiB
-// batch (config 3) ~40 % of its slot-steps carry no page.  Here each wave owns
-// a list of LIST consecutive pages and the 16 slots of k_xxh64_lds (same
-// loader / hasher lane roles, LDS hand-off and chunk arithmetic).  One step
-// moves one 256-byte segment of a page through a slot.  Before streaming, the
-// wave assigns its pages to slots greedily in list order, each to the slot
-// that frees first (argmin over 16 lanes by DPP), so every slot is busy from
-// step 0 to its own finish and the wave ends at the most loaded slot's finish
-// instead of at 16 x its longest page.  The schedule (start step and next page
-// of the same slot) sits in LDS; loads run DEPTH steps ahead of the hashing as
-// in k_xxh64_lds.  A wave still walks a window of adjacent pages: the locality
-// that size binning gave up (profiles/r01/desc_bin2_lab.txt).  Pages off the
-// lines shape (xxh64_lines_ok) get no slot; the quad kernel takes them.
-template <int MODE, bool NT, int LIST, int DEPTH>
-__global__ __launch_bounds__(256) void k_xxh64_dyn(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ len, uint64_t n,
-                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad) {
-    static_assert(LIST >= 16 && LIST <= 64, "a list fills the 16 slots; lanes hold one page each");
-    constexpr uint8_t kNone = 0xFF;
-    __shared__ __attribute__((aligned(16))) u32x4 lds[4][16][16];  // [wave][slot][16 B slot]
-    __shared__ uint64_t s_off[4][LIST];
-    __shared__ uint32_t s_len[4][LIST];    // 0: page off the lines shape (no slot)
-    __shared__ uint32_t s_start[4][LIST];  // first step of the page in its slot
-    __shared__ uint8_t s_next[4][LIST];    // next page of the same slot (kNone: last)
-    __shared__ uint8_t s_first[4][16];     // first page of each slot (kNone: idle slot)
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int r = lane >> 4, t = lane & 15;       // loader role: row r, 16-byte piece t
-    const int i = (lane >> 2) & 3, q = lane & 3;  // hasher role: slot 4i + r, quad lane q
-    const int hs = 4 * i + r;
-    const int a = q == 2 ? 3 : q == 3 ? 2 : q;
-    const uint64_t nlists = (n + LIST - 1) / LIST;
-    const uint64_t ntiles = (nlists + 3) / 4;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t L0 = ((remap ? xcd_tile(t0, ntiles) : t0) * 4 + wv) * LIST;
-        const int cnt = (int)min<uint64_t>(LIST, n > L0 ? n - L0 : 0);
-        // ---- schedule: lane p < cnt describes page L0 + p
-        uint32_t myseg = 0;
-        if (lane < cnt) {
-            const uint64_t o = off[L0 + lane];
-            const uint32_t P = len[L0 + lane];
-            const bool lines = xxh64_lines_ok(o, P);
-            s_off[wv][lane] = o;
-            s_len[wv][lane] = lines ? P : 0;
-            s_next[wv][lane] = kNone;
-            myseg = lines ? (P + 255) / 256 : 0;
-        }
-        if (lane < 16) s_first[wv][lane] = kNone;
-        uint32_t fin = 0;        // lanes 0..15: finish step of slot `lane`
-        uint32_t last = kNone;   // lanes 0..15: last page given to slot `lane`
-        for (int p = 0; p < cnt; ++p) {  // wave-uniform
-            const uint32_t ns = (uint32_t)__shfl((int)myseg, p);
-            if (ns == 0) continue;
-            // argmin over slots of (finish, slot): every lane of row 0 ends with the min
-            uint64_t key = lane < 16 ? ((uint64_t)fin << 4) | (uint32_t)lane : ~0ull;
-            key = min(key, dpp64<kRowRor1>(key));
-            key = min(key, dpp64<kRowRor2>(key));
-            key = min(key, dpp64<kRowRor4>(key));
-            key = min(key, dpp64<kRowRor8>(key));
-            const int sl = __builtin_amdgcn_readfirstlane((int)(uint32_t)key) & 15;
-            if (lane == sl) {
-                if (last == kNone) s_first[wv][sl] = (uint8_t)p;
-                else s_next[wv][last] = (uint8_t)p;
-                s_start[wv][p] = fin;
-                last = (uint32_t)p;
-                fin += ns;
-            }
-        }
-        uint32_t steps = lane < 16 ? fin : 0;  // wave's length: the busiest slot
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
-        __builtin_amdgcn_wave_barrier();
-        // ---- loader cursors (slots 4ii + r) and hasher cursor (slot hs)
-        int lc[4];
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) lc[ii] = s_first[wv][4 * ii + r];
-        int hc = s_first[wv][hs];
-        uint64_t v = xxh64_init(a), stored = 0;
-        u32x4 lastc = {0, 0, 0, 0};
-        for (uint32_t k0 = 0; k0 < steps; k0 += DEPTH) {
-            u32x4 d[DEPTH][4];
-            bool lv[DEPTH][4];
-#pragma unroll
-            for (int j = 0; j < DEPTH; ++j) {
-                const uint32_t k = k0 + j;
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii) {
-                    // advance past a finished page (a slot's pages are back to back)
-                    if (lc[ii] != kNone) {
-                        const uint32_t st = s_start[wv][lc[ii]], P = s_len[wv][lc[ii]];
-                        if (k >= st + (P + 255) / 256) lc[ii] = s_next[wv][lc[ii]];
-                    }
-                    lv[j][ii] = false;
-                    if (lc[ii] != kNone && k < steps) {
-                        const uint32_t o = 256 * (k - s_start[wv][lc[ii]]) + 16 * t;
-                        if (o < s_len[wv][lc[ii]]) {
-                            lv[j][ii] = true;
-                            d[j][ii] = ld16<NT>(reinterpret_cast<const u32x4*>(base + s_off[wv][lc[ii]] + o));
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < DEPTH; ++j) {
-                const uint32_t k = k0 + j;
-                if (k >= steps) break;  // wave-uniform
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii)
-                    if (lv[j][ii]) lds[wv][4 * ii + r][(t + 4 * ii) & 15] = d[j][ii];
-                __builtin_amdgcn_wave_barrier();
-                if (hc != kNone) {
-                    const uint32_t hlen = s_len[wv][hc];
-                    const int K = (int)(hlen / 64);
-                    const int seg = (int)(k - s_start[wv][hc]);
-#pragma unroll
-                    for (int kq = 0; kq < 4; ++kq) {
-                        const int kk = 4 * seg + kq;
-                        if (kk < K) {
-                            const u32x4 e = lds[wv][hs][(4 * kq + q + 4 * i) & 15];
-                            if (kk == 0) stored = dpp64<quad_bcast(0)>(lo64(e));
-                            if (kk == 0 || kk == K - 1)
-                                xxh64_chunk<true>(v, e, q, q == 2 && kk == 0, q != 2 && kk == K - 1);
-                            else xxh64_chunk<false>(v, e, q, false, false);
-                            if (kk == K - 1) lastc = e;
-                        }
-                    }
-                    if (4 * (seg + 1) >= K) {  // page done (whole quad): merge, 24-byte tail, avalanche
-                        const uint64_t v0 = dpp64<quad_bcast(0)>(v);
-                        const uint64_t v1 = dpp64<quad_bcast(1)>(v);
-                        const uint64_t v2 = dpp64<quad_bcast(3)>(v);
-                        const uint64_t v3 = dpp64<quad_bcast(2)>(v);
-                        uint64_t h = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
-                        h = (h ^ xxh64_round(0, v0)) * kP64_1 + kP64_4;
-                        h = (h ^ xxh64_round(0, v1)) * kP64_1 + kP64_4;
-                        h = (h ^ xxh64_round(0, v2)) * kP64_1 + kP64_4;
-                        h = (h ^ xxh64_round(0, v3)) * kP64_1 + kP64_4;
-                        h += (uint64_t)(hlen - 8);
-                        const uint64_t t0w = dpp64<quad_bcast(2)>(hi64(lastc));
-                        const uint64_t t1w = dpp64<quad_bcast(3)>(lo64(lastc));
-                        const uint64_t t2w = dpp64<quad_bcast(3)>(hi64(lastc));
-                        h ^= xxh64_round(0, t0w);
-                        h = rotl64(h, 27) * kP64_1 + kP64_4;
-                        h ^= xxh64_round(0, t1w);
-                        h = rotl64(h, 27) * kP64_1 + kP64_4;
-                        h ^= xxh64_round(0, t2w);
-                        h = rotl64(h, 27) * kP64_1 + kP64_4;
-                        h = xxh64_avalanche(h);
-                        if (q == 0)
-                            emit(MODE, L0 + hc, h, stored, const_cast<uint8_t*>(base + s_off[wv][hc]), out, ok,
-                                 first_bad);
-                        hc = s_next[wv][hc];
-                        v = xxh64_init(a);
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // the schedule arrays are rewritten by the next list
-    }
-}
-
 __device__ __forceinline__ bool xxh64_fast_ok(uint64_t off, uint32_t P) {
     return (P % 8u) == 0 && P >= 40u && (off % 8u) == 0;
 }
@@ -1656,7 +1492,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 17;
+constexpr int kTuneKeys = 16;
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1666,8 +1502,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*descriptor pages in 4 KiB slices*/ 0,
                                           /*manifest: wide block sums + chain kernel*/ 1,
                                           /*xxh64 descriptor tiles sorted by page size*/ 0,
-                                          /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4,
-                                          /*xxh64 descriptor slots refilled from lists of 32/64 pages (0 = off)*/ 0};
+                                          /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
@@ -1902,21 +1737,7 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
 #undef L
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
-            const int64_t dyn = g_tune[16].load(std::memory_order_relaxed);
-            if (xxh64_lds_layout() && dyn > 0) {
-                // slots refilled from per-wave lists of 32 or 64 pages
-                const uint64_t list = dyn >= 64 ? 64 : 32;
-                const unsigned dgrid = (unsigned)std::min<uint64_t>(((n + list - 1) / list + 3) / 4, 0x7FFFFFFFull);
-#define LD(NT_, LIST_) hipLaunchKernelGGL((k_xxh64_dyn<MODE, NT_, LIST_, 2>), dim3(dgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
-                if (use_nt()) {
-                    if (list == 64) LD(true, 64);
-                    else LD(true, 32);
-                } else {
-                    if (list == 64) LD(false, 64);
-                    else LD(false, 32);
-                }
-#undef LD
-            } else if (xxh64_lds_layout()) {
+            if (xxh64_lds_layout()) {
                 if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
                 else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
                 // pages off the lines shape are left to the quad kernel below

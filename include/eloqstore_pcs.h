@@ -237,11 +237,7 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     each 64-page tile to the four waves in
  *                                     order of page size (measured slower)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
- *                                     kernel (1, 2 or 4; 16 pages per wave)
- *   PCS_TUNE_XXH64_DYN            [0] XXH64 descriptor batches: 32 or 64 =
- *                                     each wave walks a list of that many
- *                                     pages, refilling a slot as soon as its
- *                                     page ends (0 = fixed 16-page waves) */
+ *                                     kernel (1, 2 or 4; 16 pages per wave) */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -258,7 +254,6 @@ enum pcs_tune_key {
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_DESC_SORT = 14,
     PCS_TUNE_XXH64_WAVES = 15,
-    PCS_TUNE_XXH64_DYN = 16,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

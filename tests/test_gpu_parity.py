@@ -157,18 +157,8 @@ def test_mixed_desc(golden, algo):
 
 
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
-@pytest.mark.parametrize("x64_dyn", [0, 32])
-def test_desc_odd_shapes(algo, x64_dyn):
+def test_desc_odd_shapes(algo):
     # unaligned offsets, odd lengths, pages shorter than the header, mixed with fast-path pages
-    saved = pcs.get_tuning(pcs.TUNE_XXH64_DYN)
-    pcs.set_tuning(pcs.TUNE_XXH64_DYN, x64_dyn)
-    try:
-        _desc_odd_shapes(algo)
-    finally:
-        pcs.set_tuning(pcs.TUNE_XXH64_DYN, saved)
-
-
-def _desc_odd_shapes(algo):
     rng = np.random.default_rng(7)
     lens = np.array([4096, 4100, 7, 8, 9, 100, 255, 256, 257, 1023, 1024, 8192, 3, 0, 65536, 4096, 300, 16384],
                     dtype=np.uint32)

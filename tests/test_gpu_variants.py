@@ -36,14 +36,12 @@ VARIANTS = {
     "x64_desc_sort_depth1": {pcs.TUNE_XXH64_DESC_SORT: 1, pcs.TUNE_XXH64_LAYOUT: 2},
     "x64_one_wave": {pcs.TUNE_XXH64_WAVES: 1},
     "x64_two_waves_depth4": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 4},
-    "x64_dyn32": {pcs.TUNE_XXH64_DYN: 32},
-    "x64_dyn64": {pcs.TUNE_XXH64_DYN: 64},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = list(range(1, 17))
+    keys = list(range(1, 16))
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -76,7 +74,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_quad",
                                    "desc_sort", "desc_split", "x64_desc_sort", "x64_desc_sort_depth1", "x64_one_wave",
-                                   "x64_two_waves_depth4", "x64_dyn32", "x64_dyn64"],
+                                   "x64_two_waves_depth4"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):

@@ -53,7 +53,6 @@ def main():
     ap.add_argument("--dsplit", default="0", help="XXH3 descriptor pages in 4 KiB slices (1) or not (0, the product default)")
     ap.add_argument("--x64-sort", default="0", help="XXH64 descriptor tiles sorted by size (1) or not (0)")
     ap.add_argument("--x64-waves", default="4", help="XXH64 LDS kernel waves per workgroup (PCS_TUNE_XXH64_WAVES)")
-    ap.add_argument("--x64-dyn", default="0", help="XXH64 descriptor slot refill lists (PCS_TUNE_XXH64_DYN: 0, 32, 64)")
     ap.add_argument("--b2b", type=int, default=0, help="time K back-to-back launches per sample (0 = one launch)")
     ap.add_argument("--lib", default=None, help="library to load instead of eloqstore_amd/libeloqstore_pcs.so")
     ap.add_argument("--raw-alloc", action="store_true", help="pages from a plain hipMalloc, not torch's allocator")
@@ -96,13 +95,12 @@ def main():
             splits = [int(x) for x in args.split.split(",")] if algo == 0 else [0]
             sorts = ([(a, b) for a in [int(x) for x in args.sort.split(",")] for b in [int(x) for x in args.dsplit.split(",")]]
                      if algo == 0 else [(a, w) for a in [int(x) for x in args.x64_sort.split(",")]
-                                        for w in [int(x) for x in args.x64_waves.split(",")]
-                                        + [100 + int(x) for x in args.x64_dyn.split(",") if int(x)]])
+                                        for w in [int(x) for x in args.x64_waves.split(",")]])
             for lay in layouts:
                 for sp in [(a, b) for a in splits for b in sorts]:
                     for bpc in bpcs:
                         for nt in nts:
-                            tag = (f" lay={lay}" + (" sort" if sp[1][0] else "") + (f" w={sp[1][1]}" if sp[1][1] < 100 else f" dyn={sp[1][1] - 100}") if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
+                            tag = (f" lay={lay}" + (" sort" if sp[1][0] else "") + f" w={sp[1][1]}" if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
                                    + (" sort" if sp[1][0] else "") + (" dsplit" if sp[1][1] else ""))
                             variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
                                              (lay, sp)))
@@ -118,8 +116,7 @@ def main():
             pcs.set_tuning(pcs.TUNE_DESC_SORT, srt if algo == 0 else 0)
             set_tuning_if_known(pcs.TUNE_XXH64_DESC_SORT, srt if algo == 1 else 0)
             pcs.set_tuning(pcs.TUNE_DESC_SPLIT, dsp if algo == 0 else 0)
-            set_tuning_if_known(pcs.TUNE_XXH64_WAVES, dsp if algo == 1 and 0 < dsp < 100 else 4)
-            set_tuning_if_known(pcs.TUNE_XXH64_DYN, dsp - 100 if algo == 1 and dsp >= 100 else 0)
+            set_tuning_if_known(pcs.TUNE_XXH64_WAVES, dsp if algo == 1 and dsp else 4)
             if algo == 1:
                 pcs.set_tuning(pcs.TUNE_XXH64_LAYOUT, lay)
             else:
