@@ -354,28 +354,66 @@ def test_cli(tmp_path):
     assert r.returncode == 1 and "exceeds file size" in r.stderr
 
 
-def test_full_size_properties():
-    """BASELINE config 2 at full size: 1 M x 4 KiB pages device-resident.
-    Size-independent properties: stamp -> all valid; flip byte 10 of every
-    4096th page -> exactly those fail; sampled digests equal the oracle."""
-    P, n = 4096, 1 << 20
+@pytest.mark.parametrize("P,n,algo", [
+    (4096, 1 << 20, pcs.XXH3_64),    # BASELINE config 2 (fixed-size kernel)
+    (16384, 1 << 18, pcs.XXH3_64),   # 16 KiB sweep (split-page kernel)
+    (65536, 1 << 16, pcs.XXH3_64),   # config 4 shape, 4 GiB (split-page kernel)
+    (4096, 1 << 20, pcs.XXH64),      # XXH64 LDS kernel
+    (65536, 1 << 16, pcs.XXH64),     # XXH64 LDS kernel, one workgroup per 64 large pages
+])
+def test_full_size_properties(P, n, algo):
+    """4 GiB device-resident batches at the bench's shapes.  Size-independent
+    properties: stamp -> all valid; flip byte 10 of every 4096th page ->
+    exactly those fail; sampled digests equal the oracle."""
     buf = dev_pages(P, n, 0x5EED0002, 0)
-    dig = pcs.pages_digest(buf, P, n)
-    sample = np.r_[0:64, n - 64:n, 4096:n:4096]
+    dig = pcs.pages_digest(buf, P, n, algo)
+    step = max(1, n // 256)
+    sample = np.r_[0:64, n - 64:n, step:n:step]
     got = u64(dig)[sample]
     host = buf.view(-1, P)[torch.from_numpy(sample).to(DEV)].cpu().numpy()
-    assert np.array_equal(got, oracle.pages_digest(host.reshape(-1), P))
-    pcs.pages_stamp(buf, P, n)
+    assert np.array_equal(got, oracle.pages_digest(host.reshape(-1), P, algo))
+    pcs.pages_stamp(buf, P, n, algo)
     stored = buf.view(-1, P)[:, :8].contiguous().view(torch.int64).reshape(-1)
     assert torch.equal(stored, dig)
-    ok, fb = pcs.pages_validate(buf, P, n)
+    ok, fb = pcs.pages_validate(buf, P, n, algo)
     assert int(ok.sum()) == n and int(u64(fb)[0]) == (1 << 64) - 1
-    pcs.flip_byte(buf, P, n, every=4096, byte_offset=10)
-    ok, fb = pcs.pages_validate(buf, P, n)
+    every = 4096 if n >= 1 << 20 else 1000
+    pcs.flip_byte(buf, P, n, every=every, byte_offset=10)
+    ok, fb = pcs.pages_validate(buf, P, n, algo)
     okh = ok.cpu().numpy()
-    assert int((okh == 0).sum()) == n // 4096
-    assert np.array_equal(np.nonzero(okh == 0)[0], np.arange(0, n, 4096))
-    del buf
+    assert np.array_equal(np.nonzero(okh == 0)[0], np.arange(0, n, every))
+    assert int(u64(fb)[0]) == 0
+    del buf, dig
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+def test_full_size_mixed_config3(algo):
+    """BASELINE config 3 at full size: 1 M mixed 4/8/16 KiB pages (9.33 GiB)
+    through the descriptor kernels.  Sampled digests equal the oracle; stamp
+    -> all valid; a byte flipped in every 1000th page -> exactly those fail."""
+    n = 1 << 20
+    offs, lens, total = mixed_layout(0x5EED0003, 0, n)
+    base = torch.empty(total, dtype=torch.uint8, device=DEV)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+    pcs.gen_desc(base, d_off, d_len, n, 0x5EED0003, 0)
+    dig = u64(pcs.desc_digest(base, d_off, d_len, n, algo))
+    sample = np.r_[0:32, n - 32:n, 4099:n:4099]
+    for k in sample:
+        o, L = int(offs[k]), int(lens[k])
+        page = base[o:o + L].cpu().numpy()
+        assert int(dig[k]) == int(oracle.pages_digest(page, L, algo)[0]), k
+    pcs.desc_stamp(base, d_off, d_len, n, algo)
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert int(ok.sum()) == n
+    bad = np.arange(0, n, 1000)
+    flip = torch.from_numpy((offs[bad] + 10).astype(np.int64)).to(DEV)
+    base[flip] ^= 0x5A
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert np.array_equal(np.nonzero(ok.cpu().numpy() == 0)[0], bad)
+    assert int(u64(fb)[0]) == 0
+    del base
     torch.cuda.empty_cache()
 
 
