@@ -70,6 +70,9 @@ def ref_lib():
         so.XXH_versionNumber.restype = ctypes.c_uint
         so.ref_pages_digest.argtypes = [_vp, _sz, _sz, ctypes.c_int, _vp]
         so.ref_pages_digest.restype = None
+        if hasattr(so, "ref_desc_digest"):
+            so.ref_desc_digest.argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
+            so.ref_desc_digest.restype = None
         _ref = so
     return _ref
 
@@ -128,6 +131,18 @@ def ref_pages_digest(pages: np.ndarray, page_size: int, algo: int = 0) -> np.nda
     n = pages.nbytes // page_size
     out = np.empty(n, dtype=np.uint64)
     ref.ref_pages_digest(pages.ctypes.data, page_size, n, algo, out.ctypes.data)
+    return out
+
+
+def ref_desc_digest(base: np.ndarray, off: np.ndarray, length: np.ndarray, algo: int = 0):
+    """Reference xxHash over mixed-size pages, one call per page, or None without _ref."""
+    ref = ref_lib()
+    if ref is None or not hasattr(ref, "ref_desc_digest"):
+        return None
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    out = np.empty(len(off), dtype=np.uint64)
+    ref.ref_desc_digest(base.ctypes.data, off.ctypes.data, length.ctypes.data, len(off), algo, out.ctypes.data)
     return out
 
 

@@ -18,3 +18,13 @@ void ref_pages_digest(const void *pages, size_t page_size, size_t n_pages, int a
     for (size_t i = 0; i < n_pages; ++i, p += page_size)
         out[i] = algo ? XXH64(p + 8, page_size - 8, 0) : XXH3_64bits(p + 8, page_size - 8);
 }
+
+/* Mixed-size pages (config 3): page i is len[i] bytes at base + off[i]. */
+void ref_desc_digest(const void *base, const uint64_t *off, const uint32_t *len, size_t n, int algo, uint64_t *out)
+{
+    const uint8_t *b = (const uint8_t *)base;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *p = b + off[i];
+        out[i] = algo ? XXH64(p + 8, len[i] - 8, 0) : XXH3_64bits(p + 8, len[i] - 8);
+    }
+}

@@ -112,3 +112,17 @@ def test_oracle_vs_compiled_reference_random():
             assert oracle.xxh3_64(b) == ref.XXH3_64bits(p, L), L
             assert oracle.xxh64(b, 0) == ref.XXH64(p, L, 0), L
             assert oracle.xxh64(b, 0xDEADBEEF) == ref.XXH64(p, L, 0xDEADBEEF), L
+
+
+def test_reference_loops_match_oracle_pages_and_mixed():
+    """The reference-side per-page loops (oracle/ref_pages.c over the compiled
+    external/xxhash.c; bench.py's cpu_baseline) agree with the oracle."""
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    from workload import fill_desc
+    offs, lens, total = mixed_layout(0x5EED0003, 0, 2000)
+    host = fill_desc(0x5EED0003, 0, offs, lens, total)
+    pages = fill_pages(0x5EED0002, 0, 300, 4096).reshape(-1)
+    for algo in (0, 1):
+        assert np.array_equal(oracle.ref_desc_digest(host, offs, lens, algo), oracle.desc_digest(host, offs, lens, algo))
+        assert np.array_equal(oracle.ref_pages_digest(pages, 4096, algo), oracle.pages_digest(pages, 4096, algo))
