@@ -100,7 +100,7 @@ def main():
                 for sp in [(a, b) for a in splits for b in sorts]:
                     for bpc in bpcs:
                         for nt in nts:
-                            tag = (f" lay={lay}" + (" sort" if sp[1][0] else "") + f" w={sp[1][1]}" if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
+                            tag = (f" lay={lay}" + (f" sort{sp[1][0]}" if sp[1][0] else "") + f" w={sp[1][1]}" if algo == 1 else f" rtb={lay}" + (f" split={sp[0]}" if sp[0] else "")
                                    + (" sort" if sp[1][0] else "") + (" dsplit" if sp[1][1] else ""))
                             variants.append((f"{algo_name}{tag} bpc={bpc} nt={nt}", algo, key, bpc, nt, "hash",
                                              (lay, sp)))
