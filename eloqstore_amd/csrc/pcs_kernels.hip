@@ -1742,11 +1742,16 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
                 else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
                 // pages off the lines shape are left to the quad kernel below
             }
+            // After the LDS kernel the quad kernel only picks up the pages it
+            // left (usually none): a capped grid-stride pass over the
+            // descriptors instead of one workgroup per 64 pages (14.8 -> ~4 us
+            // on config 3, profiles/r01/desc_passes.txt).
+            const unsigned qgrid = xxh64_lds_layout() ? grid_for(n, kBlock / 4, kBlocksPerCu) : grid;
             if (use_nt64())
-                hipLaunchKernelGGL((k_xxh64_desc<MODE, true>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb,
-                                   (int)xxh64_lds_layout());
+                hipLaunchKernelGGL((k_xxh64_desc<MODE, true>), dim3(qgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok,
+                                   fb, (int)xxh64_lds_layout());
             else
-                hipLaunchKernelGGL((k_xxh64_desc<MODE, false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok,
+                hipLaunchKernelGGL((k_xxh64_desc<MODE, false>), dim3(qgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok,
                                    fb, (int)xxh64_lds_layout());
         }
         hipError_t e = hipGetLastError();
