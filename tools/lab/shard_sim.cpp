@@ -1,4 +1,4 @@
-// shard_sim.cpp — EloqStore's read-path validation under load.  Not part of the product.
+// shard_sim.cpp — EloqStore's read and write checksum paths under load.  Not part of the product.
 //
 // IouringMgr::ReadPages checks up to max_read_pages_batch = 128 pages per
 // batch (async_io_manager.cpp:353-366, kv_options.h:18-19), one shard thread
@@ -13,8 +13,12 @@
 // the stored digest (ValidateChecksum, page.cpp:25-31), linked from the
 // reference's external/xxhash.c build (oracle/_ref, test infrastructure).
 //
-// Output per (T, Q): validated pages/s, GiB/s, batch latency p50 / p99 (GPU)
-// and pages/s, GiB/s (CPU).
+// The write path (FlushBatchPages, write_task.cpp:155-167; write batches of
+// up to 256 pages, kv_options.h:70) is driven the same way with SubmitStamp
+// against the reference's SetChecksum loop.
+//
+// Output per (T, Q): pages/s, GiB/s, batch latency p50 / p99 (GPU) and
+// pages/s, GiB/s (CPU).
 //
 //   make -C tools/lab && ./tools/lab/shard_sim [seconds_per_point] [pool_GiB]
 #include "eloqstore/page_checksum.h"
@@ -38,7 +42,8 @@ using namespace eloqstore;
 namespace {
 constexpr size_t P = 4096;
 constexpr size_t kChunkPages = 1024;
-constexpr size_t kBatch = 128;
+constexpr size_t kReadBatch = 128;   // max_read_pages_batch (kv_options.h:18-19)
+constexpr size_t kWriteBatch = 256;  // write batch (kv_options.h:70)
 
 uint64_t splitmix(uint64_t& s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -52,7 +57,10 @@ struct Result {
     uint64_t bad = 0;
 };
 
-Result run_gpu(const std::vector<char*>& pool, int T, int Q, double secs) {
+// write = false: ReadPages validation (SubmitValidate); true: FlushBatchPages
+// stamping (SubmitStamp writes the digests into the pool pages).
+Result run_gpu(const std::vector<char*>& pool, int T, int Q, double secs, bool write) {
+    const size_t kBatch = write ? kWriteBatch : kReadBatch;
     std::atomic<uint64_t> pages{0}, bad{0};
     std::vector<std::vector<float>> lat(T);
     const auto t0 = Clock::now();
@@ -62,14 +70,15 @@ Result run_gpu(const std::vector<char*>& pool, int T, int Q, double secs) {
         th.emplace_back([&, k] {
             uint64_t rng = 0x5EED5EEDull + (uint64_t)k * 7919;
             std::vector<ChecksumBatch> b(Q);
-            std::vector<std::vector<const char*>> ptrs(Q, std::vector<const char*>(kBatch));
+            std::vector<std::vector<char*>> ptrs(Q, std::vector<char*>(kBatch));
             std::vector<Clock::time_point> sub(Q);
             std::vector<bool> busy(Q, false);
             uint64_t done = 0, nbad = 0;
             auto submit = [&](int i) {
                 for (auto& p : ptrs[i]) p = pool[splitmix(rng) % pool.size()];
                 sub[i] = Clock::now();
-                b[i].SubmitValidate(ptrs[i], P);
+                if (write) b[i].SubmitStamp(ptrs[i], P);
+                else b[i].SubmitValidate(std::span<const char* const>(ptrs[i].data(), kBatch), P);
                 busy[i] = true;
             };
             for (int i = 0; i < Q; ++i) submit(i);
@@ -81,7 +90,7 @@ Result run_gpu(const std::vector<char*>& pool, int T, int Q, double secs) {
                     if (!b[i].Poll()) continue;
                     const auto now = Clock::now();
                     lat[k].push_back(std::chrono::duration<float, std::micro>(now - sub[i]).count());
-                    nbad += b[i].FirstBad() != kBatch;
+                    if (!write) nbad += b[i].FirstBad() != kBatch;
                     done += kBatch;
                     busy[i] = false;
                     if (now < stop) submit(i);
@@ -105,7 +114,8 @@ Result run_gpu(const std::vector<char*>& pool, int T, int Q, double secs) {
     return r;
 }
 
-Result run_cpu(const std::vector<char*>& pool, int T, double secs) {
+Result run_cpu(const std::vector<char*>& pool, int T, double secs, bool write) {
+    const size_t kBatch = write ? kWriteBatch : kReadBatch;
     std::atomic<uint64_t> pages{0}, bad{0};
     const auto t0 = Clock::now();
     const auto stop = t0 + std::chrono::duration<double>(secs);
@@ -115,11 +125,16 @@ Result run_cpu(const std::vector<char*>& pool, int T, double secs) {
             uint64_t rng = 0xC0FFEEull + (uint64_t)k * 7919;
             uint64_t done = 0, nbad = 0;
             while (Clock::now() < stop) {
-                for (size_t j = 0; j < kBatch; ++j) {  // one ReadPages batch, page by page
-                    const char* p = pool[splitmix(rng) % pool.size()];
-                    uint64_t stored;
-                    std::memcpy(&stored, p, 8);
-                    nbad += XXH3_64bits(p + 8, P - 8) != stored;
+                for (size_t j = 0; j < kBatch; ++j) {  // one batch, page by page (page.cpp:18-31)
+                    char* p = pool[splitmix(rng) % pool.size()];
+                    const uint64_t h = XXH3_64bits(p + 8, P - 8);
+                    if (write) {
+                        std::memcpy(p, &h, 8);  // SetChecksum: EncodeFixed64
+                    } else {
+                        uint64_t stored;
+                        std::memcpy(&stored, p, 8);
+                        nbad += h != stored;
+                    }
                 }
                 done += kBatch;
             }
@@ -153,21 +168,36 @@ int main(int argc, char** argv) {
         const size_t n = std::min<size_t>(65536, pool.size() - i);
         SetChecksums(std::span<char* const>(pool.data() + i, n), P);
     }
-    std::printf("pool: %zu pages of %zu B (%.2f GiB) in %zu registered chunks; batches of %zu pages; %.1f s per point\n",
-                pool.size(), P, pool.size() * (double)P / (1u << 30), chunks, kBatch, secs);
-    std::printf("%-28s %12s %9s %9s %9s %5s\n", "mode", "pages/s", "GiB/s", "p50 us", "p99 us", "bad");
-    for (int T : {1, 2, 4, 8}) {
-        for (int Q : {1, 4, 8}) {
-            const Result r = run_gpu(pool, T, Q, secs);
-            std::printf("gpu  T=%d Q=%d                 %12.0f %9.2f %9.1f %9.1f %5llu\n", T, Q, r.pages_per_s, r.gib_s,
-                        r.p50_us, r.p99_us, (unsigned long long)r.bad);
+    std::printf("pool: %zu pages of %zu B (%.2f GiB) in %zu registered chunks; %.1f s per point\n", pool.size(), P,
+                pool.size() * (double)P / (1u << 30), chunks, secs);
+    for (bool write : {false, true}) {
+        std::printf("%s: batches of %zu pages\n", write ? "write path (SubmitStamp / SetChecksum)"
+                                                        : "read path (SubmitValidate / ValidateChecksum)",
+                    write ? kWriteBatch : kReadBatch);
+        std::printf("%-28s %12s %9s %9s %9s %5s\n", "mode", "pages/s", "GiB/s", "p50 us", "p99 us", "bad");
+        for (int T : {1, 2, 4, 8}) {
+            for (int Q : {1, 4, 8}) {
+                const Result r = run_gpu(pool, T, Q, secs, write);
+                std::printf("gpu  T=%d Q=%d                 %12.0f %9.2f %9.1f %9.1f %5llu\n", T, Q, r.pages_per_s,
+                            r.gib_s, r.p50_us, r.p99_us, (unsigned long long)r.bad);
+                std::fflush(stdout);
+            }
+            const Result c = run_cpu(pool, T, secs, write);
+            std::printf("cpu  T=%d (reference loop)     %12.0f %9.2f %9s %9s %5llu\n", T, c.pages_per_s, c.gib_s, "-",
+                        "-", (unsigned long long)c.bad);
             std::fflush(stdout);
         }
-        const Result c = run_cpu(pool, T, secs);
-        std::printf("cpu  T=%d (reference loop)     %12.0f %9.2f %9s %9s %5llu\n", T, c.pages_per_s, c.gib_s, "-", "-",
-                    (unsigned long long)c.bad);
-        std::fflush(stdout);
     }
+    // the pool must still validate after both stamping runs
+    std::vector<uint8_t> ok(65536);
+    size_t bad = 0;
+    for (size_t i = 0; i < pool.size(); i += 65536) {
+        const size_t n = std::min<size_t>(65536, pool.size() - i);
+        const size_t fb = ValidateChecksums(std::span<const char* const>(pool.data() + i, n), P, ok.data());
+        bad += fb != n;
+    }
+    std::printf("pool re-validated after stamping: %s\n", bad ? "FAILED" : "ok");
+    if (bad) return 1;
     for (auto& c : chunk) {
         UnregisterPagePool(c);
         std::free(c);
