@@ -1119,9 +1119,10 @@ __global__ __launch_bounds__(256) void k_xxh3_long(const uint8_t* __restrict__ b
 // 1 MiB chunk.
 constexpr uint32_t kManifestChunk = 1u << 20;  // kCheckSumBatchSize, root_meta.cpp:157
 constexpr int kChunkBlocks = kManifestChunk / 1024;
-// Above 256 chunks the per-chunk workgroups fill the GPU and the wide form's
-// extra block-sum traffic loses (1 GiB: 380 vs 332 us, profiles/r01/long_lab.txt).
-constexpr uint64_t kWideMaxChunks = 256;
+// With 16-byte block-sum loads (k_manifest_sums16), chains staged in LDS
+// halves and the scalar fold, the wide form wins at every size, 1 GiB
+// included (283 vs 305 us; it lost above 256 chunks before, 380 vs 332 us;
+// profiles/r01/manifest_lab.txt).
 
 __device__ __forceinline__ uint32_t manifest_chunk_len(uint64_t total, uint64_t c) {
     return (uint32_t)min((uint64_t)kManifestChunk, total - c * kManifestChunk);
@@ -1141,9 +1142,68 @@ __global__ __launch_bounds__(256) void k_manifest_sums(const uint8_t* __restrict
     if (g < 8) S[(c * kChunkBlocks + b) * 8 + g] = T;
 }
 
+// The same block sums with 16-byte loads (content 16-byte aligned).  Lane g
+// of a 16-lane group holds words 2g and 2g + 1 of each 256-byte chunk cc of a
+// 1 KiB block: stripe 4cc + g/4, accumulator lanes 2(g & 3) and 2(g & 3) + 1
+// (the page kernels' layout without their one-word page offset).  Word 2g
+// adds its multiply term to the even accumulator of pair g & 3 and its raw
+// value to the odd one; word 2g + 1 the other way round (xxhash.h:5778-5817).
+// Two row rotations (4, 8) finish the block sum of each pair.  A group
+// folds four consecutive blocks (16 loads in flight per lane).
+constexpr int kSums16Blocks = 4;  // 1 KiB blocks per group
+__global__ __launch_bounds__(256) void k_manifest_sums16(const uint8_t* __restrict__ content, uint64_t total,
+                                                        uint64_t* __restrict__ S) {
+    const uint64_t c = blockIdx.y;
+    const uint32_t L = manifest_chunk_len(total, c);
+    if (L < kLongMin) return;  // a short last chunk is hashed whole by the chain kernel
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint32_t nb = (L - 1) / 1024;
+    const uint32_t b0 = (blockIdx.x * 16 + grp) * kSums16Blocks;
+    if (b0 >= nb) return;
+    uint64_t key[4][2];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int jb = 32 * cc + 2 * g + e;  // word of the block: stripe jb / 8, lane jb % 8
+            key[cc][e] = c_keys.acc[(jb >> 3) + (jb & 7)];
+        }
+    const u32x4* in = reinterpret_cast<const u32x4*>(content + c * kManifestChunk + (size_t)b0 * 1024) + g;
+    u32x4 d[kSums16Blocks][4];
+#pragma unroll
+    for (int i = 0; i < kSums16Blocks; ++i)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+            if (b0 + i < nb) d[i][cc] = ld16<true>(in + i * 64 + cc * 16);
+#pragma unroll
+    for (int i = 0; i < kSums16Blocks; ++i) {
+        if (b0 + i >= nb) break;
+        uint64_t E = 0, O = 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const uint64_t w0 = lo64(d[i][cc]), w1 = hi64(d[i][cc]);
+            E += mul32x32(w0 ^ key[cc][0]) + w1;
+            O += mul32x32(w1 ^ key[cc][1]) + w0;
+        }
+        E += dpp64<kRowRor4>(E);
+        E += dpp64<kRowRor8>(E);
+        O += dpp64<kRowRor4>(O);
+        O += dpp64<kRowRor8>(O);
+        if (g < 4) {
+            uint64_t* r = S + (c * kChunkBlocks + b0 + i) * 8 + 2 * g;
+            r[0] = E;
+            r[1] = O;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_manifest_chain(const uint8_t* __restrict__ content, uint64_t total,
                                                        const uint64_t* __restrict__ S, uint64_t* __restrict__ h) {
-    __shared__ uint64_t sums[kChunkBlocks][8];
+    // The chunk's block sums pass through LDS in halves of 512 blocks (32 KiB),
+    // so five workgroups fit a CU and 1,024 chains run in one round (a whole
+    // 64 KiB chunk of sums allowed two per CU).
+    constexpr uint32_t kHalf = kChunkBlocks / 2;
+    __shared__ uint64_t sums[kHalf][8];
     const uint64_t c = blockIdx.x;
     const uint32_t L = manifest_chunk_len(total, c);
     const uint8_t* in8 = content + c * kManifestChunk;
@@ -1153,24 +1213,28 @@ __global__ __launch_bounds__(256) void k_manifest_chain(const uint8_t* __restric
         return;
     }
     const uint32_t nb = (L - 1) / 1024;
-    const u32x4* src = reinterpret_cast<const u32x4*>(S + c * kChunkBlocks * 8);
-    u32x4* dst = reinterpret_cast<u32x4*>(&sums[0][0]);
-    for (uint32_t i = tid; i < nb * 4; i += blockDim.x) dst[i] = src[i];  // nb blocks x 64 B
-    __syncthreads();
-    if (tid >= 64) return;
     uint64_t acc = tid < 8 ? c_init_acc[tid] : 0;
-    if (tid < 8) {
-        const uint64_t key = c_keys.scr[tid];
-        uint32_t b = 0;
-        for (; b + 8 <= nb; b += 8) {  // sums do not depend on acc: read 8 ahead
-            uint64_t v[8];
+    for (uint32_t h0 = 0; h0 < nb; h0 += kHalf) {  // trip count uniform across the workgroup
+        const uint32_t hn = min(kHalf, nb - h0);
+        const u32x4* src = reinterpret_cast<const u32x4*>(S + (c * kChunkBlocks + h0) * 8);
+        u32x4* dst = reinterpret_cast<u32x4*>(&sums[0][0]);
+        for (uint32_t i = tid; i < hn * 4; i += blockDim.x) dst[i] = src[i];  // hn blocks x 64 B
+        __syncthreads();
+        if (tid < 8) {
+            const uint64_t key = c_keys.scr[tid];
+            uint32_t b = 0;
+            for (; b + 8 <= hn; b += 8) {  // sums do not depend on acc: read 8 ahead
+                uint64_t v[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = sums[b + k][tid];
+                for (int k = 0; k < 8; ++k) v[k] = sums[b + k][tid];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) acc = xxh3_scramble(acc + v[k], key);
+                for (int k = 0; k < 8; ++k) acc = xxh3_scramble(acc + v[k], key);
+            }
+            for (; b < hn; ++b) acc = xxh3_scramble(acc + sums[b][tid], key);
         }
-        for (; b < nb; ++b) acc = xxh3_scramble(acc + sums[b][tid], key);
+        __syncthreads();  // sums is refilled by the next half
     }
+    if (tid >= 64) return;
     if (tid < 16) {  // tail block, last stripe and merge, as in k_xxh3_long
         const uint64_t* in = reinterpret_cast<const uint64_t*>(in8);
         const int nst = (int)(((L - 1) - 1024 * nb) / 64);
@@ -1191,11 +1255,35 @@ __global__ __launch_bounds__(256) void k_manifest_chain(const uint8_t* __restric
     }
 }
 
-__global__ void k_manifest_fold(const uint64_t* __restrict__ chunk_h, uint64_t nchunks, uint64_t* __restrict__ out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// The fold is a serial chain over the chunk digests.  One wave loads 64
+// digests at a time (the next batch in flight while this one is folded) and
+// walks them with readlane, so the chain waits on multiplies, not on a global
+// load per chunk (1,024 chunks: 64-75 us -> see profiles/r01/manifest_lab.txt).
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+__global__ __launch_bounds__(64) void k_manifest_fold(const uint64_t* __restrict__ chunk_h, uint64_t nchunks,
+                                                     uint64_t* __restrict__ out) {
+    const int lane = threadIdx.x;
     uint64_t agg = 0;
-    for (uint64_t i = 0; i < nchunks; ++i) agg = (rotl64(agg, 1) ^ chunk_h[i]) * 0x9e3779b97f4a7c15ull;
-    *out = agg;
+    uint64_t cur = (uint64_t)lane < nchunks ? chunk_h[lane] : 0;
+    for (uint64_t b = 0; b < nchunks; b += 64) {
+        const uint64_t nb = b + 64 + (uint64_t)lane;
+        const uint64_t nxt = nb < nchunks ? chunk_h[nb] : 0;
+        const int m = (int)min<uint64_t>(64, nchunks - b);
+        // rotl by shifts, not rotl64: the rotate would be a VALU v_alignbit and a
+        // round trip out of the scalar unit on every step of the chain
+        if (m == 64) {
+#pragma unroll 16
+            for (int k = 0; k < 64; ++k) agg = (((agg << 1) | (agg >> 63)) ^ readlane64(cur, k)) * 0x9e3779b97f4a7c15ull;
+        } else {
+            for (int k = 0; k < m; ++k) agg = (((agg << 1) | (agg >> 63)) ^ readlane64(cur, k)) * 0x9e3779b97f4a7c15ull;
+        }
+        cur = nxt;
+    }
+    if (lane == 0) *out = agg;
 }
 
 __global__ void k_make_chunks(uint64_t total, uint64_t chunk, uint64_t n, uint64_t* __restrict__ off,
@@ -1780,14 +1868,18 @@ hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hip
     constexpr uint64_t kChunk = kManifestChunk;
     if (len == 0) return hipMemsetAsync(out, 0, 8, s);
     const uint64_t n = (len + kChunk - 1) / kChunk;
-    if (n <= kWideMaxChunks && ((uintptr_t)content % 8) == 0 && g_tune[13].load(std::memory_order_relaxed) != 0) {
+    if (((uintptr_t)content % 8) == 0 && g_tune[13].load(std::memory_order_relaxed) != 0) {
         // wide form: block sums over the whole GPU, then one chain per chunk
         ScratchLease scratch(s);  // block sums (64 KiB per chunk) + chunk digests
         hipError_t e = scratch.get(n * kChunkBlocks * 64 + n * 8);
         if (e != hipSuccess) return e;
         uint64_t* S = static_cast<uint64_t*>(scratch.p);
         uint64_t* h = S + n * kChunkBlocks * 8;
-        hipLaunchKernelGGL(k_manifest_sums, dim3(kChunkBlocks / 16, (unsigned)n), dim3(256), 0, s, content, len, S);
+        if ((uintptr_t)content % 16 == 0)
+            hipLaunchKernelGGL(k_manifest_sums16, dim3(kChunkBlocks / (16 * kSums16Blocks), (unsigned)n), dim3(256), 0, s,
+                               content, len, S);
+        else
+            hipLaunchKernelGGL(k_manifest_sums, dim3(kChunkBlocks / 16, (unsigned)n), dim3(256), 0, s, content, len, S);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_manifest_chain, dim3((unsigned)n), dim3(256), 0, s, content, len, S, h);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -229,10 +229,9 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     16 KiB are hashed in 4 KiB slices dealt
  *                                     to the groups round by round; 0 = one
  *                                     group walks each page (measured faster)
- *   PCS_TUNE_MANIFEST_WIDE        [1] manifests of <= 256 chunks at 8-byte
- *                                     alignment: block sums over the whole GPU
- *                                     then one chain per chunk (0 = one
- *                                     workgroup per chunk)
+ *   PCS_TUNE_MANIFEST_WIDE        [1] manifests at 8-byte alignment: block
+ *                                     sums over the whole GPU, then one chain
+ *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_DESC_SORT      [0] XXH64 descriptor batches: 1 = hand
  *                                     each 64-page tile to the four waves in
  *                                     order of page size (measured slower)
