@@ -1191,8 +1191,8 @@ __global__ __launch_bounds__(256) void k_manifest_sums16(const uint8_t* __restri
         O += dpp64<kRowRor8>(O);
         if (g < 4) {
             uint64_t* r = S + (c * kChunkBlocks + b0 + i) * 8 + 2 * g;
-            r[0] = E;
-            r[1] = O;
+            r[0] = E;  // plain stores: the chain kernel reads them back from cache
+            r[1] = O;  // (nt: sums 182 -> 186 us, chains 55 -> 74 us at 1 GiB)
         }
     }
 }
