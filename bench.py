@@ -351,7 +351,7 @@ def batch_latency(pool, pageable, w: Workload):
             ts = []
             for _ in range(200):
                 t0 = time.perf_counter()
-                fn(ptrs.ctypes.data, w.P, nb, w.algo, ok.ctypes.data, ctypes.byref(fb))
+                fn(ptrs.ctypes.data, w.P, nb, w.algo, ok.ctypes.data, ctypes.byref(fb), 0)
                 ts.append(time.perf_counter() - t0)
             row[name] = round(float(np.median(ts[20:])) * 1e6, 1)
         b = pcs.Batch()

@@ -51,7 +51,7 @@ _SIGS = {
     "pcs_desc_stamp_dev": [_vp, _vp, _vp, _u64, _i32, _vp],
     "pcs_xxh3_64_ranges_dev": [_vp, _vp, _vp, _u64, _vp, _vp],
     "pcs_xxh64_ranges_dev": [_vp, _vp, _vp, _u64, _u64, _vp, _vp],
-    "pcs_pages_validate_host": [_vp, _u64, _u64, _i32, _vp, _vp],
+    "pcs_pages_validate_host": [_vp, _u64, _u64, _i32, _vp, _vp, _u32],
     "pcs_pages_stamp_host": [_vp, _u64, _u64, _i32],
     "pcs_pages_digest_host": [_vp, _u64, _u64, _i32, _vp],
     "pcs_shard_range": [_u64, _i32, _i32, _P(_u64), _P(_u64)],
@@ -65,7 +65,7 @@ _SIGS = {
     "pcs_host_register": [_vp, _u64],
     "pcs_host_unregister": [_vp],
     "pcs_batch_create": [_P(_vp)],
-    "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32],
+    "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32, _u32],
     "pcs_batch_poll": [_vp],
     "pcs_batch_wait": [_vp],
     "pcs_batch_result": [_vp, _vp, _vp, _vp],
@@ -294,20 +294,20 @@ class Batch:
         self._keep = None
         self.n = 0
 
-    def submit(self, mode: int, pages: list, page_size: int, algo: int = XXH3_64) -> None:
+    def submit(self, mode: int, pages: list, page_size: int, algo: int = XXH3_64, skip_verify: bool = False) -> None:
         arr, keep = _page_ptrs(pages)
         self._keep = (arr, keep)
         self.n = len(pages)
         self.mode = mode
-        _call("pcs_batch_submit", self._b, mode, arr, page_size, len(pages), algo)
+        _call("pcs_batch_submit", self._b, mode, arr, page_size, len(pages), algo, _flags(skip_verify))
 
-    def submit_ptrs(self, mode: int, ptrs, page_size: int, algo: int = XXH3_64) -> None:
+    def submit_ptrs(self, mode: int, ptrs, page_size: int, algo: int = XXH3_64, skip_verify: bool = False) -> None:
         """Submit raw page addresses (a uint64 array of host pointers)."""
         ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
         self._keep = ptrs
         self.n = len(ptrs)
         self.mode = mode
-        _call("pcs_batch_submit", self._b, mode, ptrs.ctypes.data, page_size, len(ptrs), algo)
+        _call("pcs_batch_submit", self._b, mode, ptrs.ctypes.data, page_size, len(ptrs), algo, _flags(skip_verify))
 
     def poll(self) -> bool:
         rc = lib().pcs_batch_poll(self._b)
@@ -342,6 +342,14 @@ class Batch:
 
 # ---- host-memory forms (reference call surface) ------------------------------
 
+FLAG_NONE, FLAG_SKIP_VERIFY = 0, 1  # pcs_flags
+
+
+def _flags(skip_verify: bool) -> int:
+    """KvOptions::skip_verify_checksum (kv_options.h:41) -> PCS_FLAG_SKIP_VERIFY."""
+    return FLAG_SKIP_VERIFY if skip_verify else FLAG_NONE
+
+
 def _page_ptrs(pages: list) -> tuple:
     bufs = [p if isinstance(p, ctypes.Array) else (ctypes.c_char * len(p)).from_buffer(p) for p in pages]
     arr = (ctypes.c_void_p * len(bufs))(*[ctypes.addressof(b) for b in bufs])
@@ -359,16 +367,16 @@ def validate_checksum(page) -> bool:
     buf = page if isinstance(page, bytearray) else bytearray(page)
     arr, _keep = _page_ptrs([buf])
     ok = (ctypes.c_uint8 * 1)()
-    _call("pcs_pages_validate_host", arr, len(buf), 1, XXH3_64, ok, None)
+    _call("pcs_pages_validate_host", arr, len(buf), 1, XXH3_64, ok, None, FLAG_NONE)
     return bool(ok[0])
 
 
-def validate_checksums(pages: list, page_size: int, algo: int = XXH3_64):
+def validate_checksums(pages: list, page_size: int, algo: int = XXH3_64, skip_verify: bool = False):
     """Batched ValidateChecksum over scattered host pages -> (ok list, first_bad or None)."""
     arr, _keep = _page_ptrs(pages)
-    ok = (ctypes.c_uint8 * len(pages))()
+    ok = (ctypes.c_uint8 * max(1, len(pages)))()
     fb = ctypes.c_uint64(0)
-    _call("pcs_pages_validate_host", arr, page_size, len(pages), algo, ok, ctypes.byref(fb))
+    _call("pcs_pages_validate_host", arr, page_size, len(pages), algo, ok, ctypes.byref(fb), _flags(skip_verify))
     return list(ok), (None if fb.value == (1 << 64) - 1 else fb.value)
 
 
@@ -395,12 +403,13 @@ def host_unregister(addr: int) -> None:
     _call("pcs_host_unregister", addr)
 
 
-def validate_ptrs(ptrs, page_size: int, algo: int = XXH3_64):
+def validate_ptrs(ptrs, page_size: int, algo: int = XXH3_64, skip_verify: bool = False):
     """pcs_pages_validate_host over raw host page addresses -> (ok array, first_bad or None)."""
     ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
     ok = np.zeros(max(1, len(ptrs)), dtype=np.uint8)
     fb = ctypes.c_uint64(0)
-    _call("pcs_pages_validate_host", ptrs.ctypes.data, page_size, len(ptrs), algo, ok.ctypes.data, ctypes.byref(fb))
+    _call("pcs_pages_validate_host", ptrs.ctypes.data, page_size, len(ptrs), algo, ok.ctypes.data, ctypes.byref(fb),
+          _flags(skip_verify))
     return ok[: len(ptrs)], (None if fb.value == (1 << 64) - 1 else fb.value)
 
 

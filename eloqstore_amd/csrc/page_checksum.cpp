@@ -11,6 +11,10 @@
 namespace eloqstore {
 namespace {
 
+// Digest header width: eloqstore::checksum_bytes (include/storage/page.h:11),
+// which this library's public header deliberately does not define.
+constexpr size_t kChecksumBytes = 8;
+
 [[noreturn]] void die(const char* where, int rc) {
     std::fprintf(stderr, "eloqstore page checksum: %s failed (%d): %s\n", where, rc, pcs_last_error());
     std::abort();
@@ -19,30 +23,27 @@ namespace {
 }  // namespace
 
 void SetChecksum(std::string_view blob) {
-    if (blob.size() < checksum_bytes) return;
+    if (blob.size() < kChecksumBytes) return;
     void* page = const_cast<char*>(blob.data());
     if (int rc = pcs_pages_stamp_host(&page, blob.size(), 1, PCS_XXH3_64)) die("SetChecksum", rc);
 }
 
 bool ValidateChecksum(std::string_view blob) {
-    if (blob.size() < checksum_bytes) return false;
+    if (blob.size() < kChecksumBytes) return false;
     const void* page = blob.data();
     uint8_t ok = 0;
-    if (int rc = pcs_pages_validate_host(&page, blob.size(), 1, PCS_XXH3_64, &ok, nullptr))
+    if (int rc = pcs_pages_validate_host(&page, blob.size(), 1, PCS_XXH3_64, &ok, nullptr, PCS_FLAG_NONE))
         die("ValidateChecksum", rc);
     return ok != 0;
 }
 
 size_t ValidateChecksums(std::span<const char* const> pages, size_t page_size, uint8_t* ok_out, PageHash hash,
                          bool skip_verify) {
-    if (skip_verify) {
-        std::memset(ok_out, 1, pages.size());
-        return pages.size();
-    }
     uint64_t first_bad = UINT64_MAX;
     static_assert(sizeof(const char*) == sizeof(const void*));
     if (int rc = pcs_pages_validate_host(reinterpret_cast<const void* const*>(pages.data()), page_size, pages.size(),
-                                         static_cast<int>(hash), ok_out, &first_bad))
+                                         static_cast<int>(hash), ok_out, &first_bad,
+                                         skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
         die("ValidateChecksums", rc);
     return first_bad == UINT64_MAX ? pages.size() : static_cast<size_t>(first_bad);
 }
@@ -73,13 +74,15 @@ ChecksumBatch::ChecksumBatch() {
 
 ChecksumBatch::~ChecksumBatch() { pcs_batch_destroy(batch_); }
 
-void ChecksumBatch::SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash) {
+void ChecksumBatch::SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash,
+                                   bool skip_verify) {
     n_ = pages.size();
     validate_ = true;
     collected_ = false;
     ok_.assign(n_, 0);
     if (int rc = pcs_batch_submit(batch_, PCS_BATCH_VALIDATE, reinterpret_cast<const void* const*>(pages.data()),
-                                  page_size, n_, static_cast<int>(hash)))
+                                  page_size, n_, static_cast<int>(hash),
+                                  skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
         die("ChecksumBatch::SubmitValidate", rc);
 }
 
@@ -88,7 +91,7 @@ void ChecksumBatch::SubmitStamp(std::span<char* const> pages, size_t page_size, 
     validate_ = false;
     collected_ = false;
     if (int rc = pcs_batch_submit(batch_, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(pages.data()),
-                                  page_size, n_, static_cast<int>(hash)))
+                                  page_size, n_, static_cast<int>(hash), PCS_FLAG_NONE))
         die("ChecksumBatch::SubmitStamp", rc);
 }
 

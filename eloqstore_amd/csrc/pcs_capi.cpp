@@ -237,16 +237,44 @@ struct HostCtx {
 
 thread_local std::unordered_map<int, HostCtx> t_ctx;
 
-// True when pages[0..n) are one contiguous run in pinned host memory.
+// True when pages[0..n) are one contiguous run inside ONE pinned host
+// allocation: a run starting in a registered region must end inside it;
+// otherwise both the first and the last byte must be pinned host memory of
+// the same allocation (hipMemGetAddressRange).  A run that starts in a pinned
+// buffer and runs past its end, or spans two adjacent allocations, is
+// gathered instead.
 bool contiguous_pinned(const void* const* pages, uint64_t n, uint64_t P) {
     if (n == 0) return false;
     const uint8_t* base = static_cast<const uint8_t*>(pages[0]);
     for (uint64_t i = 1; i < n; ++i)
         if (pages[i] != base + i * P) return false;
-    hipPointerAttribute_t attr{};
-    const bool pinned = hipPointerGetAttributes(&attr, base) == hipSuccess && attr.type == hipMemoryTypeHost;
+    const uint8_t* last = base + n * P - 1;
+    {
+        // Regions this library registered or allocated have known extents
+        // (hipMemGetAddressRange does not resolve hipHostRegister'ed memory).
+        std::shared_lock lk(g_reg_mu);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(base);
+        auto it = g_regions.upper_bound(a);
+        if (it != g_regions.begin()) {
+            const auto& [rb, r] = *std::prev(it);
+            if (a < rb + r.bytes) return reinterpret_cast<uintptr_t>(last) < rb + r.bytes;
+        }
+    }
+    auto pinned_alloc = [](const uint8_t* p, uintptr_t* alloc_base, size_t* alloc_size) {
+        hipPointerAttribute_t attr{};
+        if (hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeHost) return false;
+        hipDeviceptr_t b = nullptr;
+        size_t sz = 0;
+        if (hipMemGetAddressRange(&b, &sz, const_cast<uint8_t*>(p)) != hipSuccess || !b || !sz) return false;
+        *alloc_base = reinterpret_cast<uintptr_t>(b);
+        *alloc_size = sz;
+        return true;
+    };
+    uintptr_t b0 = 0, b1 = 0;
+    size_t s0 = 0, s1 = 0;
+    const bool ok = pinned_alloc(base, &b0, &s0) && pinned_alloc(last, &b1, &s1) && b0 == b1 && s0 == s1;
     (void)hipGetLastError();
-    return pinned;
+    return ok;
 }
 
 // Gather scattered host pages into pinned staging.  Large chunks are split
@@ -319,16 +347,26 @@ int ensure_slot(Slot& s, size_t page_bytes, size_t n) {
     return PCS_OK;
 }
 
-// mode 0: digests -> out_dig;  mode 1: verdicts -> out_ok (+ first_bad);
-// mode 2: digests stamped into the caller's pages.
-int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* out_ok,
-               uint64_t* first_bad, uint64_t* out_dig) {
-    if (int rc = require_device()) return rc;
+int check_flags(uint32_t flags) {
+    return (flags & ~uint32_t(PCS_FLAG_SKIP_VERIFY)) ? fail(PCS_ERR_INVALID, "unknown flag bits") : PCS_OK;
+}
+
+// Argument checks shared by the synchronous and asynchronous host batches.
+int check_host_batch_args(const void* const* pages, uint64_t P, uint64_t n, int algo) {
     if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
     if (P < 8 || P > 0xFFFFFFFFull) return fail(PCS_ERR_INVALID, "page_size must be in [8, 2^32)");
     if (n && !pages) return fail(PCS_ERR_INVALID, "pages is null");
     for (uint64_t i = 0; i < n; ++i)
         if (!pages[i]) return fail(PCS_ERR_INVALID, "null page pointer in batch");
+    return PCS_OK;
+}
+
+// mode 0: digests -> out_dig;  mode 1: verdicts -> out_ok (+ first_bad);
+// mode 2: digests stamped into the caller's pages.
+int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* out_ok,
+               uint64_t* first_bad, uint64_t* out_dig) {
+    if (int rc = require_device()) return rc;
+    if (int rc = check_host_batch_args(pages, P, n, algo)) return rc;
     if (first_bad) *first_bad = UINT64_MAX;
     if (n == 0) return PCS_OK;
     int dev = 0;
@@ -438,11 +476,15 @@ int manifest_host(const void* content, uint64_t len, uint64_t* out) {
     Slot& slot = t_ctx[dev].slot[0];  // the calling thread's stream on this device
     if (int rc = ensure_slot(slot, 0, 1)) return rc;
     hipStream_t s = slot.stream;
-    void* buf = nullptr;  // [digest word | content]
+    // [content | pad to 16 | digest word]: the content starts at the
+    // buffer's base (hipMalloc alignment), so the 16-byte-load block-sum
+    // kernel (k_manifest_sums16) serves the host API too.
+    const uint64_t dig_off = (len + 15) & ~uint64_t(15);
+    void* buf = nullptr;
     int id = -1;
-    e = pcs::scratch_acquire(8 + len, &buf, &id);
-    uint64_t* d_out = static_cast<uint64_t*>(buf);
-    uint8_t* d = static_cast<uint8_t*>(buf) + 8;
+    e = pcs::scratch_acquire(dig_off + 8, &buf, &id);
+    uint8_t* d = static_cast<uint8_t*>(buf);
+    uint64_t* d_out = reinterpret_cast<uint64_t*>(d + dig_off);
     if (e == hipSuccess && len) e = hipMemcpyAsync(d, content, len, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = pcs::run_manifest(d, len, d_out, s);
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, 8, hipMemcpyDeviceToHost, s);
@@ -566,8 +608,15 @@ int pcs_xxh64_ranges_dev(const void* d_base, const uint64_t* d_off, const uint32
 }
 
 int pcs_pages_validate_host(const void* const* pages, uint64_t page_size, uint64_t n_pages, int algo, uint8_t* ok,
-                            uint64_t* first_bad) {
+                            uint64_t* first_bad, uint32_t flags) {
     if (n_pages && !ok) return fail(PCS_ERR_INVALID, "ok is null");
+    if (int rc = check_flags(flags)) return rc;
+    if (flags & PCS_FLAG_SKIP_VERIFY) {  // kv_options.h:41: the validate loop is not run
+        if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
+        if (n_pages) std::memset(ok, 1, n_pages);
+        if (first_bad) *first_bad = UINT64_MAX;
+        return PCS_OK;
+    }
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
 }
 
@@ -657,15 +706,21 @@ int pcs_batch_create(pcs_batch** out) {
     return PCS_OK;
 }
 
-int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo) {
+int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo,
+                     uint32_t flags) {
     if (!b) return fail(PCS_ERR_INVALID, "batch is null");
     if (b->state == 1) return fail(PCS_ERR_INVALID, "batch already in flight");
+    // From here on the previous batch's results are gone: a submit that fails
+    // below leaves the batch idle, so poll/wait/result refuse instead of
+    // reporting the last batch's verdicts.
+    b->state = 0;
+    b->n = 0;
+    b->first_bad = UINT64_MAX;
     if (mode < 0 || mode > 2) return fail(PCS_ERR_INVALID, "bad batch mode");
-    if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
-    if (P < 8 || P > 0xFFFFFFFFull) return fail(PCS_ERR_INVALID, "page_size must be in [8, 2^32)");
-    if (n && !pages) return fail(PCS_ERR_INVALID, "pages is null");
-    for (uint64_t i = 0; i < n; ++i)
-        if (!pages[i]) return fail(PCS_ERR_INVALID, "null page pointer in batch");
+    if (int rc = check_flags(flags)) return rc;
+    if ((flags & PCS_FLAG_SKIP_VERIFY) && mode != PCS_BATCH_VALIDATE)
+        return fail(PCS_ERR_INVALID, "PCS_FLAG_SKIP_VERIFY applies to validate batches only");
+    if (int rc = check_host_batch_args(pages, P, n, algo)) return rc;
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
     hipError_t e = hipSuccess;
@@ -697,10 +752,12 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
     b->mode = mode;
     b->n = n;
     b->P = P;
+    b->zero_copy = false;
     b->stamp_pages.assign(n, nullptr);
     if (mode == PCS_BATCH_STAMP)
         for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
-    if (n == 0) {
+    if (n == 0 || (flags & PCS_FLAG_SKIP_VERIFY)) {  // nothing to hash: complete at submit
+        if (n) std::memset(b->h_ok, 1, n);
         b->state = 2;
         b->first_bad = UINT64_MAX;
         return PCS_OK;

@@ -1503,12 +1503,16 @@ public:
             const hipError_t q = hipEventQuery(b.done);
             if (q == hipErrorNotReady) continue;
             if (q != hipSuccess) return q;
-            if (b.bytes < bytes) {
-                if (b.bytes > kKeepBytes) {  // idle and oversized: give it back
+            // An idle buffer above kKeepBytes serves only a request of at least
+            // half its size; any other request gives it back, so one large
+            // manifest or stamp does not pin its scratch for the process life.
+            const bool fits = b.bytes >= bytes && (b.bytes <= kKeepBytes || 2 * bytes >= b.bytes);
+            if (!fits) {
+                if (b.bytes > kKeepBytes) {
                     (void)hipFree(b.p);
                     b.p = nullptr;
                     b.bytes = 0;
-                    empty = (int)i;
+                    if (empty < 0) empty = (int)i;
                 }
                 continue;
             }

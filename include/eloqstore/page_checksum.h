@@ -1,10 +1,15 @@
 // page_checksum.h — C++ drop-in for EloqStore's page checksum call surface,
 // backed by the MI355X kernels behind include/eloqstore_pcs.h.
 //
-// Reference surface (namespace eloqstore, include/storage/page.h:11,25-26):
-//     constexpr uint8_t checksum_bytes = 8;
+// Reference surface (namespace eloqstore, include/storage/page.h:25-26):
 //     void SetChecksum(std::string_view blob);      // src/storage/page.cpp:18-23
 //     bool ValidateChecksum(std::string_view blob);  // src/storage/page.cpp:25-31
+// This header only re-declares those two functions (an identical
+// redeclaration is legal next to page.h) and defines nothing page.h defines:
+// the header constants (checksum_bytes = 8, page_type_offset, page.h:11-12)
+// stay page.h's, so both headers can be included in one translation unit
+// (tests/test_integration_compile.py compiles INTEGRATION.md's call-site
+// snippets against the reference's own page.h).
 // Same names, namespace and argument meaning: blob is one whole page,
 // blob.size() >= 8 is assumed exactly as in the reference (a shorter blob
 // never validates and SetChecksum leaves it untouched); SetChecksum writes the
@@ -28,8 +33,6 @@ struct pcs_batch;  // include/eloqstore_pcs.h (global namespace, C ABI)
 
 namespace eloqstore {
 
-inline constexpr uint8_t checksum_bytes = 8;  // include/storage/page.h:11
-
 void SetChecksum(std::string_view blob);
 bool ValidateChecksum(std::string_view blob);
 
@@ -41,7 +44,7 @@ enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 // (the reference loop stops at the first failure, async_io_manager.cpp:357-363;
 // the batch checks all and reports the first).  skip_verify mirrors
 // KvOptions::skip_verify_checksum (kv_options.h:41): nothing is hashed and every
-// page is reported valid.
+// page is reported valid (PCS_FLAG_SKIP_VERIFY; needs no GPU).
 size_t ValidateChecksums(std::span<const char* const> pages, size_t page_size, uint8_t* ok_out,
                          PageHash hash = PageHash::XXH3_64, bool skip_verify = false);
 
@@ -69,7 +72,10 @@ public:
     ChecksumBatch(const ChecksumBatch&) = delete;
     ChecksumBatch& operator=(const ChecksumBatch&) = delete;
 
-    void SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
+    // skip_verify mirrors KvOptions::skip_verify_checksum (kv_options.h:41):
+    // the batch completes at submit with every page reported valid.
+    void SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64,
+                        bool skip_verify = false);
     void SubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
     bool Poll();  // true once complete; never blocks
     void Wait();

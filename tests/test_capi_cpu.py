@@ -11,6 +11,7 @@ import ctypes
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 import eloqstore_amd as pcs
@@ -118,3 +119,26 @@ def test_counters_and_tuning_defaults():
     assert pcs.get_tuning(pcs.TUNE_STAMP_BYTES) == 0
     assert pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES) == 8192
     assert pcs.get_tuning(pcs.TUNE_INLINE_LIST) == 1
+
+
+def test_skip_verify_flag_needs_no_gpu():
+    """PCS_FLAG_SKIP_VERIFY mirrors KvOptions::skip_verify_checksum
+    (kv_options.h:41): the reference skips the validate loop entirely
+    (async_io_manager.cpp:239, 353), so nothing is hashed: every verdict is 1,
+    first_bad is UINT64_MAX, and the call succeeds even without a GPU.  The
+    arguments are still checked."""
+    pages = [bytearray(4096) for _ in range(5)]  # all-zero pages never validate
+    ok, fb = pcs.validate_checksums(pages, 4096, skip_verify=True)
+    assert ok == [1] * 5 and fb is None
+    ok, fb = pcs.validate_ptrs(np.zeros(0, dtype=np.uint64), 4096, skip_verify=True)
+    assert len(ok) == 0 and fb is None
+    so = pcs.lib()
+    arr, _keep = pcs._page_ptrs(pages)
+    okb = (ctypes.c_uint8 * 5)()
+    fbv = ctypes.c_uint64()
+    assert so.pcs_pages_validate_host(arr, 4096, 5, 7, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
+    assert so.pcs_pages_validate_host(arr, 4, 5, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
+    assert so.pcs_pages_validate_host(arr, 4096, 5, 0, okb, ctypes.byref(fbv), 2) == pcs.PCS_ERR_INVALID
+    assert b"unknown flag" in so.pcs_last_error()
+    nulls = (ctypes.c_void_p * 2)(arr[0], None)
+    assert so.pcs_pages_validate_host(nulls, 4096, 2, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID

@@ -1,0 +1,26 @@
+"""Runs INTEGRATION.md's call-site snippets on the GPU (built by
+tests/cpp/gen_integration.py in the build container, where the reference's
+page.h exists; the binary travels with the tree).
+
+The binary drives the ReadPages validate loop (sync and async, registered pool
+and heap pages, a corrupted page at index 77, skip_verify_checksum), and the
+WritePage / FlushBatchPages stamping in append and non-append mode, with the
+CPU oracle checking every stamped header."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "integration_snippets")
+
+pytestmark = pytest.mark.gpu
+
+
+def test_integration_snippets_run():
+    assert os.path.exists(BIN), "tests/cpp/integration_snippets missing: run __graft_entry__.build() with the reference tree present"
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "integration ok" in r.stdout
+    assert "read path source=registered: ok" in r.stdout and "read path source=heap: ok" in r.stdout
+    assert "write path append=1: 256 pages stamped" in r.stdout

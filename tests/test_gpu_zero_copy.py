@@ -140,3 +140,63 @@ def test_register_rejects_overlap_and_bad_unregister():
             pcs.host_register(pool.base + 4096, 4096)
         with pytest.raises(pcs.PcsError):
             pcs.host_unregister(pool.base + 4096)
+
+
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_pinned_run_that_overruns_its_allocation_is_gathered(zero_copy):
+    """a contiguous run that starts in pinned (registered) memory
+    and runs past the end of that allocation must not be DMA'd as one pinned
+    range: both ends are checked and must belong to one allocation."""
+    P = 4096
+    with pcs.PagePool(64, P, register=False) as pool:
+        pool.pages[:] = oracle.fill_pages(P, 64, 9).reshape(64, P)
+        want = oracle.pages_digest(pool.pages, P)
+        pcs.host_register(pool.base, 32 * P)  # only the first half is pinned
+        old = pcs.get_tuning(pcs.TUNE_ZERO_COPY)
+        try:
+            pcs.set_tuning(pcs.TUNE_ZERO_COPY, zero_copy)
+            direct0 = pcs.counter(pcs.COUNTER_DIRECT_DMA_CHUNKS)
+            dig, zc, g = _zc_delta(lambda: pcs.digest_ptrs(pool.ptr(np.arange(64)), P))
+            assert zc == 0 and g == 1 and pcs.counter(pcs.COUNTER_DIRECT_DMA_CHUNKS) == direct0
+            assert np.array_equal(dig, want)
+            # the pinned half alone is one allocation: direct (or zero-copy)
+            direct0 = pcs.counter(pcs.COUNTER_DIRECT_DMA_CHUNKS)
+            dig, zc, g = _zc_delta(lambda: pcs.digest_ptrs(pool.ptr(np.arange(32)), P))
+            assert g == 0 and (zc == 1 if zero_copy else pcs.counter(pcs.COUNTER_DIRECT_DMA_CHUNKS) == direct0 + 1)
+            assert np.array_equal(dig, want[:32])
+        finally:
+            pcs.set_tuning(pcs.TUNE_ZERO_COPY, old)
+            pcs.host_unregister(pool.base)
+
+
+def test_batch_skip_verify_and_failed_submit():
+    """skip_verify_checksum (kv_options.h:41) on the async batch, and ADVICE
+    r01: a submit that fails after a completed batch leaves the batch idle, so
+    poll/result refuse instead of returning the previous batch's verdicts."""
+    P = 4096
+    with pcs.PagePool(16, P) as pool:
+        pool.pages[:] = oracle.fill_pages(P, 16, 4).reshape(16, P)  # never stamped: all invalid
+        b = pcs.Batch()
+        b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(np.arange(16)), P)
+        b.wait()
+        ok, fb = b.result()
+        assert ok == [0] * 16 and fb == 0
+        b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(np.arange(16)), P, skip_verify=True)
+        assert b.poll()  # complete at submit
+        ok, fb = b.result()
+        assert ok == [1] * 16 and fb is None
+        with pytest.raises(pcs.PcsError):  # skip applies to validate only
+            b.submit_ptrs(pcs.Batch.STAMP, pool.ptr(np.arange(16)), P, skip_verify=True)
+        with pytest.raises(pcs.PcsError):  # batch is idle now
+            b.poll()
+        with pytest.raises(pcs.PcsError):
+            b.result()
+        b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(np.arange(16)), P)
+        with pytest.raises(pcs.PcsError):
+            b.submit_ptrs(pcs.Batch.VALIDATE, np.array([pool.base, 0], dtype=np.uint64), P)  # in flight
+        b.wait()
+        with pytest.raises(pcs.PcsError):  # null page pointer
+            b.submit_ptrs(pcs.Batch.VALIDATE, np.array([pool.base, 0], dtype=np.uint64), P)
+        with pytest.raises(pcs.PcsError):
+            b.result()
+        b.close()

@@ -217,7 +217,7 @@ int bulk(bool stamp, const char* path, const char* size_s) {
         ptrs[s].resize(cnt);
         for (uint64_t i = 0; i < cnt; ++i) ptrs[s][i] = b + i * P;
         if (pcs_batch_submit(batch[s], stamp ? PCS_BATCH_STAMP : PCS_BATCH_VALIDATE, ptrs[s].data(), P, cnt,
-                             PCS_XXH3_64)) {
+                             PCS_XXH3_64, PCS_FLAG_NONE)) {
             rc = 1;
             break;
         }
