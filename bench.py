@@ -8,22 +8,35 @@ pages already resident in HBM; value = page bytes hashed by ALL ranks per
 second (GiB/s, 2^30), per-GPU work fixed (weak scaling: every rank owns its
 own disjoint page range, no collective on the data path).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6|7]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5|6|7]
 
-Default (N=1) = BASELINE config 2: 1,048,576 x 4 KiB pages (4 GiB) per GPU.
-Configs 6/7 are the north star's 8/16 KiB page-size sweep (4 GiB per GPU).
-Multi-GPU: launched by torch.distributed.run, one process per GPU; gloo is the
-control plane (barrier + max over ranks of the timed region).
+Workload: N=1 defaults to BASELINE config 2 (1,048,576 x 4 KiB pages, 4 GiB);
+N>1 (torch.distributed.run, one process per GPU) defaults to BASELINE config 5
+(8 M x 4 KiB pages = 32 GiB per GPU, 64 M pages over 8 GPUs); gloo is the
+control plane (barrier + max over ranks of the timed region).  Configs 6/7 are
+the north star's 8/16 KiB page-size sweep (4 GiB per GPU).  --config 1 runs
+only the CPU reference over the 1 GiB file (BASELINE configs[0]).
 
 Also reported, on the same line:
   roofline      dominant kernel's algorithmic bytes per launch / average launch
                 time (HIP events on the launch stream) vs 8 TB/s HBM peak;
-                traffic = PMC-measured HBM bytes per launch when a matching
-                rocprofv3 summary is committed under profiles/ (else null).
-  read_ceiling  the same load pattern with the hash removed (achievable rate).
-  cpu_baseline  the reference's own xxHash (oracle/_ref, one XXH3_64bits call
-                per page like page.cpp:18-31) on ONE host core over a bounded
-                sample of the same pages; its digests double as a parity check.
+                traffic = PMC-measured HBM bytes per launch from the committed
+                rocprofv3 summary under profiles/ (else null).
+  read_ceiling  a plain streaming read of the same buffer (no hash).
+  cpu_baseline  BASELINE config 1: the reference's own xxHash (oracle/_ref) on
+                ONE host thread, reading every page of a 1 GiB file of 4 KiB
+                pages and validating it like page_checksum_tool / page.cpp:25-31;
+                cpu_all_cores: the same over all usable host cores; cli_scan:
+                this repo's GPU CLI (--scan) over the same file.
+  parity        sampled GPU digests (every 4096th page, first/last 64) against
+                the reference xxHash on the host.
+  sweep         (N=1) every other BASELINE config and mode, one entry each:
+                config 3 (XXH3 and XXH64), config 4, config 5, config 7 (16 KiB),
+                config 2 validate (read path) and stamp (write path), each with
+                its avg launch time, roofline frac, parity sample and
+                corruption drill.
+  scaling       (N>1) per-rank wall and kernel-event times, and efficiency =
+                per-GPU rate / rank 0's rate on the same shard run alone.
 """
 from __future__ import annotations
 
@@ -147,7 +160,7 @@ class Workload:
         validate (all pass), flip byte 10 of every `every`-th page, validate:
         exactly those must fail and the first bad index must be 0."""
         if self.P is None:
-            return None
+            return self._desc_drill(every)
         pcs.pages_stamp(self.pages, self.P, self.n, self.algo)
         pcs.pages_validate(self.pages, self.P, self.n, self.algo, ok=self.ok, first_bad=self.fb)
         clean = int(self.ok.sum().item())
@@ -159,6 +172,25 @@ class Workload:
         pcs.flip_byte(self.pages, self.P, self.n, every=every, byte_offset=10)  # restore
         return {"pages": self.n, "valid_after_stamp": clean, "flipped": flipped, "detected": detected,
                 "first_bad": first, "pass": clean == self.n and detected == flipped and first == 0}
+
+    def _desc_drill(self, every: int):
+        pcs.desc_stamp(self.pages, self.d_off, self.d_len, self.n, self.algo)
+        pcs.desc_validate(self.pages, self.d_off, self.d_len, self.n, self.algo, ok=self.ok, first_bad=self.fb)
+        clean = int(self.ok.sum().item())
+        idx = self.d_off[::every] + 10
+        self.pages[idx] ^= 0xFF
+        pcs.desc_validate(self.pages, self.d_off, self.d_len, self.n, self.algo, ok=self.ok, first_bad=self.fb)
+        flipped = int(idx.numel())
+        detected = int((self.ok == 0).sum().item())
+        first = int(self.fb.item())
+        self.pages[idx] ^= 0xFF  # restore
+        return {"pages": self.n, "valid_after_stamp": clean, "flipped": flipped, "detected": detected,
+                "first_bad": first, "pass": clean == self.n and detected == flipped and first == 0}
+
+    def free(self):
+        for k in ("pages", "out", "ok", "fb", "d_off", "d_len"):
+            if hasattr(self, k):
+                delattr(self, k)
 
     def algorithmic_bytes(self, mode: str = "digest") -> int:
         # every page byte read once (the 8-byte header shares the first line) + the result written:
@@ -195,52 +227,39 @@ class Workload:
         return None
 
 
-def cpu_baseline(w: Workload, target_s: float):
-    """Reference xxHash on one host core over a bounded sample of the same pages."""
-    import oracle  # test/baseline infrastructure only (see oracle/__init__.py)
+def parity_sample(w: Workload, mode: str = "digest"):
+    """Sampled parity against the reference xxHash on the host:
+    pages 0..63, every 4096th page and the last 64.  digest/validate: the
+    GPU's digests of those pages (w.out, written by a digest step); stamp: the
+    8-byte headers the stamp wrote into the pages."""
+    import oracle  # checker only
 
-    if w.P is None:
-        from workload import fill_desc
-        k = 16384
-        host = fill_desc(w.seed, w.first, w.offs[:k], w.lens[:k], int(w.offs[k - 1]) + int(w.lens[k - 1]))
-        gpu = w.out[:k].cpu().numpy().view(np.uint64)
-        ref = oracle.ref_desc_digest(host, w.offs[:k], w.lens[:k], w.algo) is not None
-        fn = oracle.ref_desc_digest if ref else oracle.desc_digest
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            want = fn(host, w.offs[:k], w.lens[:k], w.algo)
-            reps += 1
-            if time.perf_counter() - t0 >= target_s:
-                break
-        dt = time.perf_counter() - t0
-        what = ("reference external/xxhash.c v0.8.3 (gcc -O2, SSE2 path), one call per page" if ref
-                else "oracle C restatement, one call per page")
-        return {"value": reps * host.nbytes / dt / GIB, "unit": "GiB/s", "cores": 1,
-                "kind": "reference" if ref else "port",
-                "sample": f"first {k} mixed pages ({host.nbytes / 2**20:.0f} MiB) of the batch x {reps} passes; {what}"}, \
-            {"pages": k, "mismatches": int((want != gpu).sum())}
-    host, P, gpu = w.sample_pages_host(256 << 20)
-    fn = oracle.ref_pages_digest if oracle.ref_lib() is not None else None
-    kind = "reference" if fn else "port"
-    if fn is None:
-        fn = oracle.pages_digest
-    want = fn(host, P, w.algo)
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        fn(host, P, w.algo)
-        reps += 1
-        if time.perf_counter() - t0 >= target_s:
-            break
-    dt = time.perf_counter() - t0
-    what = ("reference external/xxhash.c v0.8.3 (gcc -O2, SSE2 path), one XXH3_64bits call per page"
-            if kind == "reference" else "oracle C restatement, one call per page")
-    if w.algo == pcs.XXH64:
-        what = what.replace("XXH3_64bits", "XXH64")
-    return {"value": reps * host.nbytes / dt / GIB, "unit": "GiB/s", "cores": 1, "kind": kind,
-            "sample": f"first {host.nbytes // P} pages ({host.nbytes >> 20} MiB) of the batch x {reps} passes; {what}"}, \
-        {"pages": int(host.nbytes // P), "mismatches": int((want != gpu).sum())}
+    idx = np.unique(np.concatenate([np.arange(min(64, w.n)), np.arange(0, w.n, 4096),
+                                    np.arange(max(0, w.n - 64), w.n)])).astype(np.int64)
+    tidx = torch.from_numpy(idx).to(w.dev)
+    if w.P is not None:
+        host = w.pages.view(w.n, w.P).index_select(0, tidx).cpu().numpy()
+        fn = oracle.ref_pages_digest if oracle.ref_lib() is not None else oracle.pages_digest
+        want = fn(host.reshape(-1), w.P, w.algo)
+    else:
+        offs, lens = w.offs[idx], w.lens[idx]
+        parts = [w.pages[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
+        host = torch.cat(parts).cpu().numpy()
+        new_off = np.zeros(len(idx), dtype=np.uint64)
+        np.cumsum(lens[:-1], dtype=np.uint64, out=new_off[1:])
+        want = oracle.ref_desc_digest(host, new_off, lens, w.algo)
+        if want is None:
+            want = oracle.desc_digest(host, new_off, lens, w.algo)
+    if mode == "stamp":
+        if w.P is not None:
+            got = host[:, :8].copy().view(np.uint64).ravel()
+        else:
+            got = np.array([host[int(o):int(o) + 8].view(np.uint64)[0] for o in new_off], dtype=np.uint64)
+    else:
+        got = w.out.index_select(0, tidx).cpu().numpy().view(np.uint64)
+    checker = "reference external/xxhash.c (oracle/_ref)" if oracle.ref_lib() is not None else "oracle C restatement"
+    return {"pages": int(len(idx)), "mismatches": int((want != got).sum()), "checker": checker,
+            "what": "headers written by the stamp" if mode == "stamp" else "GPU digests"}
 
 
 def cpu_model() -> str:
@@ -253,36 +272,105 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_all_cores(w: Workload, target_s: float):
-    """The same reference loop on several host threads (disjoint page ranges of
-    the sample), for context: BASELINE.md's all-cores CPU figure."""
+def usable_cores() -> int:
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
+def cgroup_cpu_quota():
+    """CPUs this process may use per the cgroup v2 quota (None if unlimited)."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
+CONFIG1_SEED = 0x5EED0001
+CONFIG1_PAGES = 1 << 18  # 1 GiB of 4 KiB pages (SURVEY §8d, BASELINE configs[0])
+
+
+def config1(target_s: float, all_cores_s: float | None, workdir: str | None = None):
+    """BASELINE config 1: the reference checksum over a 1 GiB file of 4 KiB
+    pages on ONE host thread (tools/page_checksum_tool.cpp reads a page from
+    the file and calls ValidateChecksum, page.cpp:25-31).
+
+    The file (splitmix64 pages, seed 0x5EED0001, stamped) is written by this
+    repo's CLI (`page_checksum_tool --gen`, GPU-stamped).  The timed loop is
+    oracle/_ref's ref_scan_file: pread one page, XXH3_64bits from the
+    reference's own external/xxhash.c, compare with the stored header; whole
+    passes over the file are repeated for ~target_s (page cache warm).  Every
+    page must validate: the reference agreeing with the GPU's stamps is a
+    parity check of its own.  Also: the same loop on all usable host cores
+    (disjoint page ranges, one thread each), and the repo CLI's --scan."""
+    import shutil
+    import subprocess
+    import tempfile
     import threading
 
     import oracle  # baseline infrastructure only
 
-    if w.P is None or oracle.ref_lib() is None:
-        return None
-    host, P, _ = w.sample_pages_host(256 << 20)
-    k = host.nbytes // P
-    nthreads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    parts = [host[i * k // nthreads * P:(i + 1) * k // nthreads * P] for i in range(nthreads)]
-    done = [0] * nthreads
-    stop = time.perf_counter() + target_s
+    P, n = 4096, CONFIG1_PAGES
+    d = tempfile.mkdtemp(prefix="pcs_config1_", dir=workdir)
+    path = os.path.join(d, "config1.data")
+    try:
+        r = subprocess.run([pcs.TOOL_PATH, "--gen", path, str(n), str(P), hex(CONFIG1_SEED)],
+                           capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(f"page_checksum_tool --gen failed: {r.stderr.strip()}")
+        ref = oracle.ref_lib() is not None and hasattr(oracle.ref_lib(), "ref_scan_file")
+        if not ref:
+            return None
+        oracle.ref_scan_file(path, P, 0, n)  # warm the page cache
+        passes, bad, t0 = 0, 0, time.perf_counter()
+        while True:
+            got, b = oracle.ref_scan_file(path, P, 0, n)
+            assert got == n * P
+            bad += b
+            passes += 1
+            if time.perf_counter() - t0 >= target_s:
+                break
+        dt = time.perf_counter() - t0
+        one = {"value": round(passes * n * P / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "reference",
+               "sample": f"config 1: {passes} passes over a 1 GiB file of {n} x 4 KiB pages (seed 0x5EED0001, "
+                         f"stamped by page_checksum_tool --gen), pread + reference external/xxhash.c v0.8.3 "
+                         f"XXH3_64bits (gcc -O2, SSE2) + compare per page on one thread, page cache warm",
+               "pages_failed": bad, "cpu": cpu_model()}
+        allc = None
+        if all_cores_s:
+            # one thread per core this process may actually use: the affinity
+            # mask, capped by a cgroup CPU quota when one is set (a GPU box
+            # shows every core of the host but grants a share of them)
+            quota = cgroup_cpu_quota()
+            T = usable_cores() if quota is None else max(1, min(usable_cores(), int(quota)))
+            done = [0] * T
+            fails = [0] * T
+            stop = time.perf_counter() + all_cores_s
 
-    def run(i):
-        while time.perf_counter() < stop:
-            oracle.ref_pages_digest(parts[i], P, w.algo)
-            done[i] += parts[i].nbytes
+            def run(i):
+                b0, e0 = i * n // T, (i + 1) * n // T
+                while time.perf_counter() < stop:
+                    got, b = oracle.ref_scan_file(path, P, b0, e0 - b0)
+                    done[i] += got
+                    fails[i] += b
 
-    t0 = time.perf_counter()
-    th = [threading.Thread(target=run, args=(i,)) for i in range(nthreads)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    dt = time.perf_counter() - t0
-    return {"value": round(sum(done) / dt / GIB, 2), "unit": "GiB/s", "cores": nthreads, "kind": "reference",
-            "cpu": cpu_model(), "sample": f"{k} pages split over {nthreads} threads, ~{target_s:.0f} s"}
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=run, args=(i,)) for i in range(T)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            dt = time.perf_counter() - t0
+            allc = {"value": round(sum(done) / dt / GIB, 2), "unit": "GiB/s", "cores": T, "kind": "reference",
+                    "nproc": os.cpu_count(), "usable_cores": usable_cores(), "cgroup_cpu_quota": cgroup_cpu_quota(),
+                    "cpu": cpu_model(), "pages_failed": sum(fails),
+                    "sample": f"config 1 file, {T} threads (one per usable core: affinity mask capped by the cgroup "
+                              f"CPU quota) on disjoint page ranges, "
+                              f"~{all_cores_s:.0f} s"}
+        r = subprocess.run([pcs.TOOL_PATH, "--scan", path, str(P)], capture_output=True, text=True, timeout=300)
+        scan = {"rc": r.returncode, "line": r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr.strip()}
+        return {"cpu_baseline": one, "cpu_all_cores": allc, "cli_scan": scan}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def host_inclusive(w: Workload, max_pages: int = 1 << 18):
@@ -369,6 +457,84 @@ def batch_latency(pool, pageable, w: Workload):
     return out
 
 
+def timed_launches(w: Workload, mode: str, steps: int, warmup: int) -> float:
+    """Average launch time (s) of `steps` back-to-back steps, bracketed by two
+    HIP events on the launch stream (torch's current stream)."""
+    for _ in range(warmup):
+        w.step(mode)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(steps):
+        w.step(mode)
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / 1e3 / steps
+
+
+# (entry key, BASELINE config, algo, mode): every BASELINE config and mode the
+# headline line does not cover, run by the default N=1 bench (VERDICT r01 #2).
+SWEEP = (
+    ("config3_xxh3", 3, 0, "digest"),
+    ("config3_xxh64", 3, 1, "digest"),
+    ("config4_xxh3", 4, 0, "digest"),
+    ("config5_xxh3", 5, 0, "digest"),
+    ("config7_xxh3", 7, 0, "digest"),
+    ("config2_xxh3_validate", 2, 0, "validate"),
+    ("config2_xxh3_stamp", 2, 0, "stamp"),
+)
+PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits the kernel trace on it
+
+
+def sweep(dev: str, steps: int, warmup: int):
+    out = []
+    for key, cfg, algo, mode in SWEEP:
+        w = Workload(cfg, algo, 0, None, dev)
+        if mode == "validate":
+            w.step("stamp")
+        torch.cuda.synchronize()
+        time.sleep(PHASE_GAP_S)
+        t_wall0 = time.perf_counter()
+        avg = timed_launches(w, mode, steps, warmup)
+        t_wall = time.perf_counter() - t_wall0
+        time.sleep(PHASE_GAP_S)
+        alg = w.algorithmic_bytes(mode)
+        if mode != "stamp":
+            w.step("digest")  # w.out = this batch's digests for the parity sample
+            torch.cuda.synchronize()
+        par = parity_sample(w, mode)
+        drill = w.corruption_drill()
+        traffic = committed_traffic_key(key)
+        e = {"key": key, "config": cfg, "workload": w.desc, "algo": "xxh3_64" if algo == 0 else "xxh64",
+             "mode": mode, "pages": w.n, "bytes": w.bytes, "steps": steps, "warmup": warmup,
+             "avg_launch_ms": round(avg * 1e3, 4), "GiBps": round(w.bytes / avg / GIB, 1),
+             "achieved_GBps": round(alg / avg / 1e9, 1), "frac": round(alg / avg / 1e9 / HBM_PEAK_GBPS, 4),
+             "algorithmic_bytes_per_launch": alg, "wall_s": round(t_wall, 3),
+             "traffic": traffic[0] if traffic else None, "traffic_source": traffic[1] if traffic else None,
+             "parity": par, "corruption_drill": drill}
+        out.append(e)
+        w.free()
+        del w
+        torch.cuda.empty_cache()
+        time.sleep(PHASE_GAP_S)
+    return out
+
+
+def committed_traffic_key(key: str):
+    """HBM bytes per launch for a sweep entry from the committed summary."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*sweep*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for e in d.get("entries", []):
+            if e.get("key") == key and e.get("traffic_bytes_per_launch"):
+                best = (e["traffic_bytes_per_launch"], os.path.relpath(path, ROOT))
+    return best
+
+
 def committed_traffic(cfg: int, algo: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     best = None
@@ -381,22 +547,28 @@ def committed_traffic(cfg: int, algo: int):
         key = f"config{cfg}_{'xxh3' if algo == 0 else 'xxh64'}"
         if key in d.get("traffic_bytes_per_launch", {}):
             best = (d["traffic_bytes_per_launch"][key], os.path.relpath(path, ROOT))
+    if cfg == 2 and algo == 0:
+        best = committed_traffic_key("headline") or best
     return best
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=None, choices=[1] + sorted(CONFIGS),
+                    help="default: 2 on one GPU, 5 (8M pages per GPU) when WORLD_SIZE > 1")
     ap.add_argument("--algo", choices=["xxh3", "xxh64"], default="xxh3")
     ap.add_argument("--pages-per-gpu", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["digest", "validate", "stamp"], default="digest",
                     help="digest (metric), validate (read path), stamp (write path)")
-    ap.add_argument("--all-cores", action="store_true", help="also time the CPU reference on all host threads")
+    ap.add_argument("--no-all-cores", action="store_true", help="skip the all-cores CPU reference run")
+    ap.add_argument("--no-sweep", action="store_true", help="headline only (no per-config sweep)")
+    ap.add_argument("--sweep-steps", type=int, default=50)
+    ap.add_argument("--sweep-warmup", type=int, default=5)
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the host-memory path (pinned direct DMA and pageable gather)")
     args = ap.parse_args()
@@ -404,6 +576,18 @@ def main():
     world, rank, local = dist_env()
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    if args.config == 1:  # BASELINE configs[0]: CPU reference only, runs without a GPU
+        if rank == 0:
+            c1 = config1(args.cpu_seconds, None if args.no_all_cores else min(args.cpu_seconds, 5.0))
+            one = c1["cpu_baseline"]
+            print(json.dumps({"metric": "GiB/s page_checksum_tool-style validate over a 1 GiB file of 4 KiB pages, "
+                                        "reference xxHash on one host thread",
+                              "value": one["value"], "unit": "GiB/s", "n_gpus": 0, "higher_is_better": True,
+                              "dtype": "u64", "data": "synthetic (splitmix64 pages, seed 0x5EED0001)",
+                              "config": {"workload": "config1: 1 GiB file, 4 KiB pages, single host thread"},
+                              **c1}), flush=True)
+        return
+    cfg = args.config if args.config is not None else (5 if world > 1 else 2)
     dist = init_dist(world)
     ndev = torch.cuda.device_count()
     gpu = local % max(1, ndev)  # 1:1 on a full node; ranks share a GPU only in a rehearsal
@@ -413,7 +597,7 @@ def main():
     dev = f"cuda:{gpu}"
     algo = pcs.XXH3_64 if args.algo == "xxh3" else pcs.XXH64
 
-    w = Workload(args.config, algo, rank, args.pages_per_gpu, dev)
+    w = Workload(cfg, algo, rank, args.pages_per_gpu, dev)
     if args.mode == "validate":  # the read path checks stamped pages (mostly valid)
         w.step("stamp")
         torch.cuda.synchronize()
@@ -421,6 +605,7 @@ def main():
     for _ in range(args.warmup):
         w.step(args.mode)
     torch.cuda.synchronize()
+    time.sleep(PHASE_GAP_S)
 
     # Two HIP events on the launch stream (torch's current stream) bracket the
     # K steps: the average launch duration is their span / K.  Events around
@@ -443,24 +628,53 @@ def main():
     avg_launch = ev0.elapsed_time(ev1) / 1e3 / args.steps
     total_bytes = sum_over_ranks(dist, float(w.bytes)) * args.steps
     value = total_bytes / elapsed / GIB
+    time.sleep(PHASE_GAP_S)
+
+    scaling = None
+    if dist is not None:
+        # Per-rank evidence, then rank 0 alone on its own shard (the others wait
+        # at the barrier): efficiency = concurrent per-GPU rate / solo rate.
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "gpu": gpu, "wall_s": round(t1 - t0, 5),
+                                          "kernel_event_ms_per_step": round(avg_launch * 1e3, 4),
+                                          "GiBps": round(w.bytes * args.steps / (t1 - t0) / GIB, 1)})
+        solo = None
+        barrier(dist)
+        if rank == 0:
+            torch.cuda.synchronize()
+            s0 = time.perf_counter()
+            for _ in range(args.steps):
+                w.step(args.mode)
+            torch.cuda.synchronize()
+            solo = w.bytes * args.steps / (time.perf_counter() - s0) / GIB
+        barrier(dist)
+        if rank == 0:
+            scaling = {"per_rank": per_rank, "solo_rank0_GiBps": round(solo, 1),
+                       "efficiency": round(value / world / solo, 4),
+                       "efficiency_def": "per-GPU rate of the concurrent run / rank 0's rate on the same shard "
+                                         "run alone in this job",
+                       "shared_gpus": ndev < world}
+        time.sleep(PHASE_GAP_S)
 
     if args.mode != "digest":  # leave self.out holding this batch's digests for the parity leg
         w.step("digest")
         torch.cuda.synchronize()
-    ceiling = w.read_ceiling(max(3, args.steps // 5))
-    cpu, parity, allcores = (None, None, None)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline(w, args.cpu_seconds)
-        if cpu is not None:
-            cpu["cpu"] = cpu_model()
-        if args.all_cores:
-            allcores = cpu_all_cores(w, min(args.cpu_seconds, 5.0))
+    parity = parity_sample(w) if rank == 0 else None
+    ceiling = w.read_ceiling(max(3, args.steps // 20))
+    time.sleep(PHASE_GAP_S)
     drill = w.corruption_drill() if rank == 0 else None
+    time.sleep(PHASE_GAP_S)
     hostinc = host_inclusive(w) if args.host_inclusive and rank == 0 else None
+    sweep_entries = None
+    if rank == 0 and world == 1 and not args.no_sweep:
+        sweep_entries = sweep(dev, args.sweep_steps, args.sweep_warmup)
+    c1 = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        c1 = config1(args.cpu_seconds, None if args.no_all_cores else min(args.cpu_seconds, 5.0))
 
     if rank == 0:
         achieved = w.algorithmic_bytes(args.mode) / avg_launch / 1e9
-        traffic = committed_traffic(args.config, algo) if args.mode == "digest" else None
+        traffic = committed_traffic(cfg, algo) if args.mode == "digest" else None
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -501,14 +715,19 @@ def main():
                 "launch_timing": f"HIP events bracketing the {args.steps} timed steps on the launch stream",
             },
             "read_ceiling_GBps": round(ceiling, 1) if ceiling else None,
-            "cpu_baseline": cpu,
+            "cpu_baseline": c1["cpu_baseline"] if c1 else None,
             "parity": parity,
         }
         line["corruption_drill"] = drill
-        if allcores is not None:
-            line["cpu_all_cores"] = allcores
+        if c1 is not None:
+            line["cpu_all_cores"] = c1["cpu_all_cores"]
+            line["cli_scan"] = c1["cli_scan"]
+        if scaling is not None:
+            line["scaling_detail"] = scaling
         if hostinc is not None:
             line["host_inclusive"] = hostinc
+        if sweep_entries is not None:
+            line["sweep"] = sweep_entries
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

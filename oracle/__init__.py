@@ -70,6 +70,9 @@ def ref_lib():
         so.XXH_versionNumber.restype = ctypes.c_uint
         so.ref_pages_digest.argtypes = [_vp, _sz, _sz, ctypes.c_int, _vp]
         so.ref_pages_digest.restype = None
+        if hasattr(so, "ref_scan_file"):
+            so.ref_scan_file.argtypes = [ctypes.c_char_p, _sz, _u64, _u64, _vp]
+            so.ref_scan_file.restype = ctypes.c_longlong
         if hasattr(so, "ref_desc_digest"):
             so.ref_desc_digest.argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
             so.ref_desc_digest.restype = None
@@ -156,3 +159,18 @@ def page_digest_sample(seed: int, page_size: int, page_index: int, algo: int = 0
     """Digest of synthetic page `page_index` (generator rule shared with pcs_gen_pages_dev)."""
     page = fill_pages(page_size, 1, seed, page_index)
     return int(pages_digest(page, page_size, algo)[0])
+
+
+def ref_scan_file(path: str, page_size: int, first_page: int, n_pages: int):
+    """Config 1: the reference's per-page read + ValidateChecksum loop over a
+    file range on the calling thread (oracle/ref_pages.c).  Returns (bytes read,
+    failing pages), or None without _ref.  ctypes drops the GIL for the call,
+    so Python threads scanning disjoint ranges run in parallel."""
+    ref = ref_lib()
+    if ref is None or not hasattr(ref, "ref_scan_file"):
+        return None
+    bad = ctypes.c_uint64(0)
+    got = ref.ref_scan_file(path.encode(), page_size, first_page, n_pages, ctypes.byref(bad))
+    if got < 0:
+        raise OSError(f"ref_scan_file failed on {path}")
+    return int(got), int(bad.value)

@@ -76,15 +76,25 @@ def test_two_ranks_gpu_shards_match_oracle(tmp_path):
 
 
 def test_bench_two_ranks_torchrun():
+    """The driver's scaling launch, rehearsed with 2 ranks on the box's one GPU:
+    with no --config, N>1 defaults to BASELINE config 5 (8 M x 4 KiB pages =
+    32 GiB per rank, generated in place); rank 0 prints one line with per-rank
+    wall/kernel-event times and the efficiency against its solo rate."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--pages-per-gpu", "65536"]
+           "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]  # rank 0 only
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 3
-    assert line["config"]["pages_per_gpu"] == 65536
+    assert line["config"]["workload"].startswith("config5")
+    assert line["config"]["pages_per_gpu"] == 1 << 23 and line["config"]["bytes_per_gpu"] == 32 << 30
     assert line["value"] > 0 and line["aggregate_roofline"]["peak_GBps"] == 2 * 8000.0
-    assert line["corruption_drill"]["pass"]
+    assert line["corruption_drill"]["pass"] and line["parity"]["mismatches"] == 0
+    sd = line["scaling_detail"]
+    assert [p["rank"] for p in sd["per_rank"]] == [0, 1]
+    assert all(p["kernel_event_ms_per_step"] > 0 and p["wall_s"] > 0 for p in sd["per_rank"])
+    assert sd["efficiency"] > 0 and sd["solo_rank0_GiBps"] > 0 and sd["shared_gpus"]
+    assert "sweep" not in line  # the sweep is an N=1 leg
