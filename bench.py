@@ -198,15 +198,13 @@ class Workload:
         return self.bytes + (1 if mode == "validate" else 8) * self.n
 
     def read_ceiling(self, reps: int) -> float | None:
-        scratch = torch.empty_like(self.out)  # keep self.out = the digests of the timed steps
-        if self.P is None:  # mixed sizes: the descriptor kernel's load pattern
-            def run():
-                pcs.read_ceiling_desc(self.pages, self.d_off, self.d_len, self.n, scratch)
-        elif self.P in (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
-            def run():
-                pcs.read_ceiling(self.pages, self.P, self.n, scratch)
-        else:
-            return None
+        """The same bytes read by the plain streaming-read kernel (no hash):
+        pcs_stream_read_dev over the whole batch buffer."""
+        scratch = torch.empty((self.bytes + 65535) // 65536, dtype=torch.int64, device=self.dev)
+
+        def run():
+            pcs.stream_read(self.pages, self.bytes, scratch)
+
         run()
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

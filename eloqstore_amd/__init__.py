@@ -58,8 +58,7 @@ _SIGS = {
     "pcs_gen_pages_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
     "pcs_gen_desc_dev": [_vp, _vp, _vp, _u64, _u64, _u64, _vp],
     "pcs_flip_byte_dev": [_vp, _u64, _u64, _u64, _u64, _vp],
-    "pcs_read_ceiling_dev": [_vp, _u64, _u64, _vp, _vp],
-    "pcs_read_ceiling_desc_dev": [_vp, _vp, _vp, _u64, _vp, _vp],
+    "pcs_stream_read_dev": [_vp, _u64, _vp, _vp],
     "pcs_host_alloc_pinned": [_u64, _P(_vp)],
     "pcs_host_free_pinned": [_vp],
     "pcs_host_register": [_vp, _u64],
@@ -143,17 +142,12 @@ def _stream(stream) -> int:
 TUNE_XXH3_BLOCKS_PER_CU = 1
 TUNE_XXH64_BLOCKS_PER_CU = 2
 TUNE_NT_LOADS = 3
-TUNE_XXH64_NT_LOADS = 4
-TUNE_STAMP_BYTES = 5
 TUNE_XXH64_LAYOUT = 6
 TUNE_ZERO_COPY = 7
 TUNE_XXH3_RT_BATCH = 8
 TUNE_XXH3_SPLIT_PAGES = 9
-TUNE_DESC_SORT = 10
 TUNE_INLINE_LIST = 11
-TUNE_DESC_SPLIT = 12
 TUNE_MANIFEST_WIDE = 13
-TUNE_XXH64_DESC_SORT = 14
 TUNE_XXH64_WAVES = 15
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
@@ -260,12 +254,10 @@ def flip_byte(pages, page_size: int, n: int, every: int, byte_offset: int = 10, 
     _call("pcs_flip_byte_dev", _ptr(pages), page_size, n, every, byte_offset, _stream(stream))
 
 
-def read_ceiling(pages, page_size: int, n: int, out, stream=None) -> None:
-    _call("pcs_read_ceiling_dev", _ptr(pages), page_size, n, _ptr(out), _stream(stream))
-
-
-def read_ceiling_desc(base, off, length, n: int, out, stream=None) -> None:
-    _call("pcs_read_ceiling_desc_dev", _ptr(base), _ptr(off), _ptr(length), n, _ptr(out), _stream(stream))
+def stream_read(buf, nbytes: int, out, stream=None) -> None:
+    """pcs_stream_read_dev: plain streaming read of nbytes (the read ceiling);
+    out receives one folded u64 per 64 KiB window."""
+    _call("pcs_stream_read_dev", _ptr(buf), nbytes, _ptr(out), _stream(stream))
 
 
 def manifest_checksum_host(content: bytes) -> int:

@@ -47,8 +47,8 @@ hipError_t scratch_acquire(size_t bytes, void** out, int* id);
 hipError_t scratch_release(int id, hipStream_t s);
 int set_tuning(int key, int64_t value);
 int64_t get_tuning(int key);
-hipError_t run_read_ceiling(const uint8_t* pages, uint64_t page_size, uint64_t n, uint64_t* out, hipStream_t s);
-hipError_t run_read_ceiling_desc(const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
-                                 uint64_t* out, hipStream_t s);
+// Plain streaming read of [buf, buf + bytes) (the HBM read ceiling): one
+// folded word per 64 KiB window into out[0 .. ceil(bytes / 65536)).
+hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s);
 
 }  // namespace pcs

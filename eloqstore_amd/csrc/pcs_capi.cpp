@@ -929,23 +929,14 @@ int pcs_flip_byte_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, uint6
                   "flip kernel launch");
 }
 
-int pcs_read_ceiling_dev(const void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t* d_out,
-                         pcs_stream_t stream) {
+int pcs_stream_read_dev(const void* d_buf, uint64_t bytes, uint64_t* d_out, pcs_stream_t stream) {
     if (int rc = require_device()) return rc;
-    if (n_pages && (!d_pages || !d_out)) return fail(PCS_ERR_INVALID, "null pointer");
-    const hipError_t e = pcs::run_read_ceiling(static_cast<const uint8_t*>(d_pages), page_size, n_pages, d_out,
-                                               reinterpret_cast<hipStream_t>(stream));
-    if (e == hipErrorNotSupported) return fail(PCS_ERR_INVALID, "page_size must be a power of two in [256, 65536]");
-    return finish(e, "read-ceiling kernel launch");
-}
-
-int pcs_read_ceiling_desc_dev(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint64_t n,
-                              uint64_t* d_out, pcs_stream_t stream) {
-    if (int rc = require_device()) return rc;
-    if (n && (!d_base || !d_off || !d_len || !d_out)) return fail(PCS_ERR_INVALID, "null pointer");
-    return finish(pcs::run_read_ceiling_desc(static_cast<const uint8_t*>(d_base), d_off, d_len, n, d_out,
-                                             reinterpret_cast<hipStream_t>(stream)),
-                  "read-ceiling kernel launch");
+    if (bytes && (!d_buf || !d_out)) return fail(PCS_ERR_INVALID, "null pointer");
+    if (reinterpret_cast<uintptr_t>(d_buf) % 16) return fail(PCS_ERR_INVALID, "d_buf must be 16-byte aligned");
+    const hipError_t e = pcs::run_stream_read(static_cast<const uint8_t*>(d_buf), bytes, d_out,
+                                              reinterpret_cast<hipStream_t>(stream));
+    if (e == hipErrorNotSupported) return fail(PCS_ERR_INVALID, "bytes too large (more than 2^31 windows)");
+    return finish(e, "stream-read kernel launch");
 }
 
 }  // extern "C"

@@ -42,14 +42,15 @@ namespace pcs {
 // blocks sharing an XCD (blockIdx % 8) stream one contiguous slice of the
 // batch (cdna_hip_programming.md T1, bijective form); measured +1 %.
 //
-// Stamp (SetChecksum) rewrites the first stamp_bytes of the page from the
-// registers that already hold them, with the digest in bytes [0, 8): a bare
-// 8-byte store per page is a partial-line write the memory side must merge
-// (measured -26 % vs digest mode); whole-line rewrites avoid the merge.
+// Digest and validate only: a stamp (SetChecksum) is this kernel's digest
+// pass followed by k_scatter_stamp (pages_impl), because header writes
+// interleaved with the read stream cost 20 % at every rewrite width
+// (the in-place forms were retired in round 2).
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   unsigned long long* first_bad, int stamp_bytes) {
+                                                   unsigned long long* first_bad) {
+    static_assert(MODE != kStamp, "stamps run as digest + k_scatter_stamp");
     __shared__ uint64_t tile_h[16];
     __shared__ uint8_t tile_ok[16];
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
@@ -64,39 +65,26 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
             uint64_t stored = 0;
             u32x4 first;
             const uint64_t h = xxh3_page_fixed<P, NT>(page, L, stored, first);
-            if (MODE == kStamp) {
-                if (stamp_bytes <= 8) {
-                    if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
-                } else if (L.g * 16 < stamp_bytes) {
-                    if (L.g == 0) {
-                        first.x = (uint32_t)h;
-                        first.y = (uint32_t)(h >> 32);
-                        if (out) st_nt(out + pg, h);
-                    }
-                    st_nt(reinterpret_cast<u32x4*>(const_cast<uint8_t*>(page)) + L.g, first);
-                }
-            } else if (L.g == 0) {
+            if (L.g == 0) {
                 tile_h[grp] = h;
                 tile_ok[grp] = (h == stored) ? 1 : 0;
             }
         }
-        if (MODE != kStamp) {
-            __syncthreads();
-            const uint64_t i = t * 16 + threadIdx.x;
-            if (threadIdx.x < 16 && i < n) {
-                if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
-                if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
-            }
-            if (MODE == kValidate && first_bad && threadIdx.x == 0) {
-                // one note per tile: its smallest failing page
-                for (int k = 0; k < 16 && t * 16 + k < n; ++k)
-                    if (!tile_ok[k]) {
-                        note_bad(first_bad, t * 16 + k);
-                        break;
-                    }
-            }
-            __syncthreads();
+        __syncthreads();
+        const uint64_t i = t * 16 + threadIdx.x;
+        if (threadIdx.x < 16 && i < n) {
+            if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
+            if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
         }
+        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+            // one note per tile: its smallest failing page
+            for (int k = 0; k < 16 && t * 16 + k < n; ++k)
+                if (!tile_ok[k]) {
+                    note_bad(first_bad, t * 16 + k);
+                    break;
+                }
+        }
+        __syncthreads();
     }
 }
 
@@ -228,187 +216,32 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
     }
 }
 
-// Descriptor batch (mixed sizes).  Pages that miss the fast-path shape are
-// left to k_generic_desc.
-// Descriptor pages handled by k_xxh3_desc_split: whole 4 KiB slices, at most
-// 16 KiB (a tile of 16 pages is then at most 64 slices).
-__device__ __forceinline__ bool desc_split_ok(uint64_t off, uint32_t P) {
-    return (P % 4096u) == 0 && P >= 4096u && P <= 16384u && (off % 16u) == 0;
-}
-
-// Mixed-size descriptor batches with the split-page scheme (k_xxh3_split),
-// PCS_TUNE_DESC_SPLIT = 1.  Measured 8 % SLOWER than k_xxh3_desc on config 3
-// (6.38 vs 6.93 TB/s, profiles/r01/dsplit_lab.txt: the per-tile prefix, chain
-// and three barriers, at 3 waves per SIMD), so it is off by default:
-
-// the 4 KiB slices of a tile's 16 pages are dealt to the 16 groups in rounds,
-// 16 consecutive slices per round, so a workgroup reads 64 KiB of (packed)
-// page bytes at a time whatever the page sizes, and no group idles while a
-// neighbour walks a longer page.  Each group leaves the block sums of its
-// slice in LDS; then group i runs page i's scramble chain and merge.
-template <int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_xxh3_desc_split(const uint8_t* __restrict__ base,
-                                                        const uint64_t* __restrict__ off,
-                                                        const uint32_t* __restrict__ len, uint64_t n,
-                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                        unsigned long long* first_bad) {
-    constexpr int kMaxSlices = 64;
-    __shared__ uint64_t S[kMaxSlices * 4][4][2];  // block sums, block 4k + i of slice k
-    __shared__ uint64_t C[kMaxSlices];            // first input word of each slice (previous block's carry)
-    __shared__ uint8_t sl_page[kMaxSlices], sl_num[kMaxSlices];
-    __shared__ uint8_t first_slice[17];
-    __shared__ uint64_t stored_w[16], tile_h[16];
-    __shared__ uint8_t tile_ok[16], tile_has[16];
-    // the lane's key set is built per phase rather than kept live across the tile
-    const int grp = threadIdx.x >> 4, p = threadIdx.x & 3;
-    const uint64_t k22 = c_keys.acc[22];
-    const uint64_t ntiles = (n + 15) / 16;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        if (threadIdx.x < 16) {  // slice counts and their prefix sum (lanes 0-15 of wave 0)
-            const uint64_t i = t * 16 + threadIdx.x;
-            int cnt = 0;
-            if (i < n && desc_split_ok(off[i], len[i])) cnt = (int)(len[i] / 4096u);
-            int incl = cnt;
-#pragma unroll
-            for (int d = 1; d < 16; d <<= 1) {
-                const int v = __shfl_up(incl, d, 16);
-                if ((int)threadIdx.x >= d) incl += v;
-            }
-            const int excl = incl - cnt;
-            first_slice[threadIdx.x] = (uint8_t)excl;
-            if (threadIdx.x == 15) first_slice[16] = (uint8_t)incl;
-            for (int k = 0; k < cnt; ++k) {
-                sl_page[excl + k] = (uint8_t)threadIdx.x;
-                sl_num[excl + k] = (uint8_t)k;
-            }
-            tile_has[threadIdx.x] = cnt > 0;
-        }
-        __syncthreads();
-        const int total = first_slice[16];
-        for (int r = 0; r * 16 < total; ++r) {  // block-uniform trip count
-            const int k = r * 16 + grp;
-            if (k < total) {
-                const int i = sl_page[k], j = sl_num[k];
-                const uint64_t pg = t * 16 + i;
-                const uint32_t P = len[pg];
-                const u32x4* src = reinterpret_cast<const u32x4*>(base + off[pg] + 4096u * j) + (threadIdx.x & 15);
-                u32x4 d[4][4];
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) d[b][c] = ld16<NT>(src + b * 64 + c * 16);
-                if ((threadIdx.x & 15) == 0) {
-                    C[k] = lo64(d[0][0]);
-                    if (j == 0) stored_w[i] = lo64(d[0][0]);
-                }
-                const bool last = (j == (int)(P / 4096u) - 1);
-                const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    uint64_t Te, To;
-                    if (b < 3) xxh3_block_terms<false>(L, d[b], lo64(d[b + 1][0]), 4, Te, To);
-                    else if (!last) xxh3_block_terms<false, true>(L, d[b], 0, 4, Te, To);
-                    else xxh3_block_terms<true>(L, d[b], 0, 4, Te, To);
-                    if (L.g < 4) {
-                        S[4 * k + b][p][0] = Te;
-                        S[4 * k + b][p][1] = To;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        {  // group i: page i's chain
-            const int i = grp;
-            const uint64_t pg = t * 16 + i;
-            if (tile_has[i]) {
-                const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-                const uint32_t P = len[pg];
-                const int NB = (int)(P / 1024u) - 1, s0 = 4 * first_slice[i];
-                uint64_t Ae = L.init_e, Ao = L.init_o;
-                for (int b = 0; b < NB; ++b) {
-                    uint64_t Te = S[s0 + b][p][0], To = S[s0 + b][p][1];
-                    if ((b & 3) == 3 && p == 3) {
-                        const uint64_t cw = C[first_slice[i] + ((b + 1) >> 2)];
-                        Te += cw;
-                        To += mul32x32(cw ^ k22);
-                    }
-                    Ae = xxh3_scramble(Ae + Te, L.ks_e);
-                    Ao = xxh3_scramble(Ao + To, L.ks_o);
-                }
-                const uint64_t h = xxh3_merge(L, Ae + S[s0 + NB][p][0], Ao + S[s0 + NB][p][1], (uint64_t)(P - 8));
-                if (L.g == 0) {
-                    tile_h[i] = h;
-                    tile_ok[i] = h == stored_w[i];
-                }
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < 16 && tile_has[threadIdx.x]) {
-            const uint64_t i = t * 16 + threadIdx.x;
-            const uint64_t h = tile_h[threadIdx.x];
-            if (MODE == kStamp) {
-                st_nt(reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(base) + off[i]), h);
-                if (out) st_nt(out + i, h);
-            } else {
-                if (MODE == kDigest || out) st_nt(out + i, h);
-                if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
-            }
-        }
-        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
-            for (int k = 0; k < 16 && t * 16 + k < n; ++k)
-                if (tile_has[k] && !tile_ok[k]) {
-                    note_bad(first_bad, t * 16 + k);
-                    break;
-                }
-        }
-        __syncthreads();  // LDS is rewritten by the next tile
-    }
-}
-
-template <int MODE, bool NT, bool B4, bool SORT>
+// Descriptor batch (mixed sizes), one group per page.  Pages that miss the
+// fast-path shape are left to k_generic_desc.  Measured alternatives, all
+// bit-exact and all slower on config 3: 4 KiB slices dealt
+// to the groups in rounds (-8 %), byte-budget slice windows (-12..-30 %),
+// per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %).
+template <int MODE, bool NT, bool B4>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad, int skip_split) {
-    // SORT: the 16 pages of a tile are handed to the groups in order of size,
-    // so the four groups of a wave mostly share one size and none idles while
-    // a neighbour walks a longer page (mixed-size batches, config 3).
-    __shared__ uint8_t perm[16];
+                                                  unsigned long long* first_bad) {
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
         const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        int slot = threadIdx.x >> 4;
-        if constexpr (SORT) {
-            if (threadIdx.x < 16) {
-                const uint64_t i = t * 16 + threadIdx.x;
-                const uint32_t mine = i < n ? len[i] : 0xFFFFFFFFu;
-                int rank = 0;
-                for (int k = 0; k < 16; ++k) {
-                    const uint64_t ik = t * 16 + k;
-                    const uint32_t other = ik < n ? len[ik] : 0xFFFFFFFFu;
-                    rank += (other < mine) || (other == mine && k < (int)threadIdx.x);
-                }
-                perm[rank] = (uint8_t)threadIdx.x;
-            }
-            __syncthreads();
-            slot = perm[threadIdx.x >> 4];
-        }
-        const uint64_t pg = t * 16 + slot;
+        const uint64_t pg = t * 16 + (threadIdx.x >> 4);
         if (pg < n) {
             const uint64_t o = off[pg];
             const uint32_t P = len[pg];
-            if (xxh3_fast_ok(o, P) && !(skip_split && desc_split_ok(o, P))) {
+            if (xxh3_fast_ok(o, P)) {
                 const uint8_t* page = base + o;
                 uint64_t stored = 0;
                 const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
                 if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
             }
         }
-        if constexpr (SORT) __syncthreads();  // perm is rewritten by the next tile
     }
 }
 
@@ -543,12 +376,12 @@ __device__ __forceinline__ uint64_t xxh64_page(const uint8_t* __restrict__ page,
     return xxh64_tail(h, page + 8 + 32 * (uint64_t)ns, len);
 }
 
-// XXH64 with full-line loads (page_size % 64 == 0, 16-byte aligned page).
+// XXH64 chunk arithmetic for 64-byte pieces (page_size % 64 == 0, 16-byte
+// aligned page), used by k_xxh64_lds below.
 //
-// Lane q of a quad loads page bytes [64k + 16q, +16) of chunk k — page words
-// 8k + 2q (half e0) and 8k + 2q + 1 (e1) — so a wave-instruction reads sixteen
-// whole 64-byte pieces.  XXH64 stripe s covers page words 4s+1 .. 4s+4 and
-// accumulator a consumes page word 4s + a + 1.  Accumulators are placed as
+// Lane q of a quad holds page bytes [64k + 16q, +16) of chunk k — page words
+// 8k + 2q (half e0) and 8k + 2q + 1 (e1).  XXH64 stripe s covers page words
+// 4s+1 .. 4s+4 and accumulator a consumes page word 4s + a + 1.  Accumulators are placed as
 // lane q -> acc {0, 1, 3, 2}[q]; acc 3 runs one stripe behind (stripes 2k-1
 // and 2k per chunk).  Then each lane needs its own half of one word and its
 // partner's (q ^ 2) other half:
@@ -582,54 +415,6 @@ __device__ __forceinline__ void xxh64_chunk(uint64_t& v, u32x4 d, int q, bool sk
     }
 }
 
-template <bool NT>
-__device__ __forceinline__ uint64_t xxh64_page_lines(const uint8_t* __restrict__ page, uint32_t P, int q,
-                                                     uint64_t& stored) {
-    constexpr int U = 8;  // chunks in flight per lane (128 B per lane, 8 KiB per wave)
-    const int K = (int)(P / 64);  // >= 2
-    const u32x4* base = reinterpret_cast<const u32x4*>(page) + q;
-    const int a = q == 2 ? 3 : q == 3 ? 2 : q;
-    uint64_t v = xxh64_init(a);
-    // chunk 0: acc 3 (lane 2) has no stripe -1; page word 0 is the stored digest
-    const u32x4 d0 = ld16<NT>(base);
-    stored = dpp64<quad_bcast(0)>(lo64(d0));
-    xxh64_chunk<true>(v, d0, q, q == 2, false);
-    // chunks 1 .. K-2: no skips
-    int k = 1;
-    for (; k + U <= K - 1; k += U) {
-        u32x4 d[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) d[u] = ld16<NT>(base + 4 * (k + u));
-#pragma unroll
-        for (int u = 0; u < U; ++u) xxh64_chunk<false>(v, d[u], q, false, false);
-    }
-    for (; k < K - 1; ++k) xxh64_chunk<false>(v, ld16<NT>(base + 4 * k), q, false, false);
-    // chunk K-1: stripe 2k+1 is the 24-byte tail for accs 0-2
-    const u32x4 last = ld16<NT>(base + 4 * (K - 1));
-    xxh64_chunk<true>(v, last, q, false, q != 2);
-    // merge in accumulator order: acc 0,1,2,3 live in lanes 0,1,3,2
-    const uint64_t v0 = dpp64<quad_bcast(0)>(v);
-    const uint64_t v1 = dpp64<quad_bcast(1)>(v);
-    const uint64_t v2 = dpp64<quad_bcast(3)>(v);
-    const uint64_t v3 = dpp64<quad_bcast(2)>(v);
-    uint64_t h = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
-    h = (h ^ xxh64_round(0, v0)) * kP64_1 + kP64_4;
-    h = (h ^ xxh64_round(0, v1)) * kP64_1 + kP64_4;
-    h = (h ^ xxh64_round(0, v2)) * kP64_1 + kP64_4;
-    h = (h ^ xxh64_round(0, v3)) * kP64_1 + kP64_4;
-    h += (uint64_t)(P - 8);
-    const uint64_t t0 = dpp64<quad_bcast(2)>(hi64(last));
-    const uint64_t t1 = dpp64<quad_bcast(3)>(lo64(last));
-    const uint64_t t2 = dpp64<quad_bcast(3)>(hi64(last));
-    h ^= xxh64_round(0, t0);
-    h = rotl64(h, 27) * kP64_1 + kP64_4;
-    h ^= xxh64_round(0, t1);
-    h = rotl64(h, 27) * kP64_1 + kP64_4;
-    h ^= xxh64_round(0, t2);
-    h = rotl64(h, 27) * kP64_1 + kP64_4;
-    return xxh64_avalanche(h);
-}
-
 __device__ __forceinline__ bool xxh64_lines_ok(uint64_t off, uint32_t P) {
     return (P % 64u) == 0 && P >= 128u && (off % 16u) == 0;
 }
@@ -655,24 +440,16 @@ enum Addr : int { kAddrStride = 0, kAddrDesc = 1, kAddrList = 2 };
 
 // DEPTH segments are loaded before the first of them is hashed (DEPTH x 4 KiB
 // per wave in flight).
-// SORT (descriptor batches, PCS_TUNE_XXH64_DESC_SORT): the block's 64 pages
-// are handed to its waves in order of size, so a wave no longer walks 16 KiB
-// of segments for mostly shorter pages (~58 % of lane slots useful unsorted,
-// ~85 % sorted on config 3).  Measured 4 % SLOWER on config 3 (6.16 vs 6.42
-// TB/s, profiles/r01/x64_sort_lab.txt): the block is held until its slowest
-// (all-16 KiB) wave ends, so the idle slots move from lanes to whole waves.
-// Off by default; kept as a tested variant.
 // WPB waves per workgroup (PCS_TUNE_XXH64_WAVES): a workgroup owns 16 * WPB
-// consecutive pages.
-template <int MODE, bool NT, int ADDR, int DEPTH, bool SORT = false, int WPB = 4>
+// consecutive pages.  Sorting a tile's pages by size before handing them to
+// the waves measured 4 % slower on config 3 (profiles/r01/x64_sort_lab.txt:
+// the block is held until its all-16 KiB wave ends) and was retired in round 2.
+template <int MODE, bool NT, int ADDR, int DEPTH, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                        const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                        unsigned long long* first_bad) {
-    static_assert(!SORT || WPB == 4, "the tile sort ranks 64 pages with the block's first wave");
     __shared__ __attribute__((aligned(16))) u32x4 lds[WPB][16][16];  // [wave][page slot][16 B slot]
-    __shared__ uint32_t s_key[SORT ? 64 : 1];
-    __shared__ uint8_t s_perm[SORT ? 64 : 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = lane >> 4, t = lane & 15;        // loader role
     const int i = (lane >> 2) & 3, q = lane & 3;   // hasher role: page 4i + r, quad lane q
@@ -682,33 +459,8 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
         const uint64_t T = (remap ? xcd_tile(t0, ntiles) : t0) * kTile;
-        if constexpr (SORT) {
-            if (threadIdx.x < 64) {
-                const uint64_t pg = T + threadIdx.x;
-                uint32_t key = 0;  // pages the fast path skips sort first (no segments)
-                if (pg < n) {
-                    const uint32_t L = len[pg];
-                    key = xxh64_lines_ok(off[pg], L) ? L : 0;
-                }
-                s_key[threadIdx.x] = key;
-            }
-            __syncthreads();
-            if (threadIdx.x < 64) {
-                const uint32_t mine = s_key[threadIdx.x];
-                int rank = 0;
-                for (int k = 0; k < 64; ++k) {
-                    const uint32_t other = s_key[k];
-                    rank += (other < mine) || (other == mine && k < (int)threadIdx.x);
-                }
-                s_perm[rank] = (uint8_t)threadIdx.x;
-            }
-            __syncthreads();
-        }
         // page in wave slot j (0..15) of this wave
-        auto page_at = [&](int j) -> uint64_t {
-            const int slot = wv * 16 + j;
-            return T + (SORT ? s_perm[slot] : slot);
-        };
+        auto page_at = [&](int j) -> uint64_t { return T + wv * 16 + j; };
         // loader pages (4ii + r) and hasher page (4i + r)
         const uint8_t* lp[4];
         uint32_t lP[4];
@@ -806,7 +558,6 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
             h = xxh64_avalanche(h);
             if (q == 0) emit(MODE, hp, h, stored, const_cast<uint8_t*>(hptr), out, ok, first_bad);
         }
-        if constexpr (SORT) __syncthreads();  // s_key / s_perm are rewritten by the next tile
     }
 }
 
@@ -815,7 +566,11 @@ __device__ __forceinline__ bool xxh64_fast_ok(uint64_t off, uint32_t P) {
     return (P % 8u) == 0 && P >= 40u && (off % 8u) == 0;
 }
 
-template <int MODE, bool NT, bool LINES>
+// Pages off the 64-byte-piece shape (P % 64 != 0 or 8-byte-aligned only): one
+// quad per page, lane a reading accumulator a's words (xxh64_page).  The quad
+// layout for line-shaped pages (each quad loading its own 64 B pieces, 80 % of
+// spec) was retired in round 2 for k_xxh64_lds.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                      uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                      unsigned long long* first_bad) {
@@ -827,16 +582,17 @@ __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict_
         if (pg >= n) continue;
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
-        const uint64_t h = LINES ? xxh64_page_lines<NT>(page, P, a, stored) : xxh64_page<false>(page, P, a, stored);
+        const uint64_t h = xxh64_page<false>(page, P, a, stored);
         if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
 
-template <int MODE, bool NT>
+// Descriptor pages k_xxh64_lds leaves (fast XXH64 shape, not line-shaped).
+template <int MODE>
 __global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                    const uint32_t* __restrict__ len, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   unsigned long long* first_bad, int skip_lines) {
+                                                   unsigned long long* first_bad) {
     const int a = threadIdx.x & 3;
     const uint64_t ntiles = (n + 63) / 64;
     const bool remap = gridDim.x == ntiles;
@@ -845,11 +601,10 @@ __global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ 
         if (pg >= n) continue;
         const uint64_t o = off[pg];
         const uint32_t P = len[pg];
-        if (!xxh64_fast_ok(o, P) || (skip_lines && xxh64_lines_ok(o, P))) continue;
+        if (!xxh64_fast_ok(o, P) || xxh64_lines_ok(o, P)) continue;
         const uint8_t* page = base + o;
         uint64_t stored = 0;
-        const uint64_t h = xxh64_lines_ok(o, P) ? xxh64_page_lines<NT>(page, P, a, stored)
-                                                : xxh64_page<false>(page, P, a, stored);
+        const uint64_t h = xxh64_page<false>(page, P, a, stored);
         if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
@@ -1350,98 +1105,49 @@ __global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pag
     if (i < n) st_nt(reinterpret_cast<uint64_t*>(pages + i * P), dig[i]);
 }
 
-// Same loads, tile order and staged result stores as k_xxh3_fixed<P, kDigest>
-// (or, SPLIT, as k_xxh3_split<P, kDigest>: G = P / 4096 groups per page, one
-// 4 KiB slice each) with the hash replaced by an xor/add fold: the achievable
-// rate of the product's layout (the roofline's "measured ceiling").
-// Read ceiling for descriptor batches: page pg (off[pg], len[pg] with
-// len % 256 == 0, 16-byte aligned; others are skipped) read by one 16-lane
-// group like xxh3_page_rt4 — 16 nt loads of 16 B per lane per 4 KiB step —
-// folded with xor/add, one 8-byte result per page staged per tile.
-template <bool NT>
-__global__ __launch_bounds__(256) void k_read_ceiling_desc(const uint8_t* __restrict__ base,
-                                                          const uint64_t* __restrict__ off,
-                                                          const uint32_t* __restrict__ len, uint64_t n,
-                                                          uint64_t* __restrict__ out) {
-    __shared__ uint64_t tile_r[16];
+// Streaming-read ceiling: the fastest plain read of a device byte range found
+// (tools/lab/stream_lab.hip, profiles/r02/read_ceiling_lab.txt): one-shot
+// workgroups over contiguous 64 KiB windows in XCD-contiguous order, the
+// product's lane layout (16-lane groups over 4 KiB slices, 16 nt dwordx4 loads
+// per lane issued before any is used), folded with xor/add into one word per
+// window.  7.2-7.3 TB/s over 4-32 GiB, insensitive to workgroups per CU (2-8)
+// and window size (32-128 KiB); the hash kernels on 4 KiB pages reach
+// 7.3-7.45 TB/s, i.e. they run AT the practical read ceiling of the part.
+constexpr uint64_t kStreamWin = 65536;
+__global__ __launch_bounds__(256) void k_stream_read(const uint8_t* __restrict__ buf, uint64_t bytes,
+                                                    uint64_t* __restrict__ out) {
+    const uint64_t nwin = (bytes + kStreamWin - 1) / kStreamWin;
+    const uint64_t w = xcd_tile(blockIdx.x, nwin);
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const uint64_t ntiles = (n + 15) / 16;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        const uint64_t pg = t * 16 + grp;
-        uint64_t r = 0;
-        if (pg < n) {
-            const uint64_t o = off[pg];
-            const uint32_t P = len[pg];
-            if (xxh3_fast_ok(o, P)) {
-                const u32x4* p = reinterpret_cast<const u32x4*>(base + o) + g;
-                const uint32_t steps = P / 4096, rest = (P % 4096) / 256;
-                uint32_t x = 0, y = 0, z = 0, w = 0;
-                for (uint32_t k = 0; k < steps; ++k) {
-                    u32x4 d[16];
+    const uint8_t* win = buf + w * kStreamWin + 4096u * grp + 16u * g;
+    const uint64_t lim = bytes - w * kStreamWin;  // bytes of this window (full ones: >= 64 KiB)
+    u32x4 d[16];
 #pragma unroll
-                    for (int c = 0; c < 16; ++c) d[c] = ld16<NT>(p + (k * 16 + c) * 16);
-#pragma unroll
-                    for (int c = 0; c < 16; ++c) { x ^= d[c].x; y += d[c].y; z ^= d[c].z; w += d[c].w; }
-                }
-                for (uint32_t c = 0; c < rest; ++c) {
-                    const u32x4 v = ld16<NT>(p + (steps * 16 + c) * 16);
-                    x ^= v.x; y += v.y; z ^= v.z; w += v.w;
-                }
-                r = ((uint64_t)(x ^ z) << 32) | (y + w);
-            }
-        }
-        r ^= dpp64<kRowRor1>(r);
-        r ^= dpp64<kRowRor2>(r);
-        r ^= dpp64<kRowRor4>(r);
-        r ^= dpp64<kRowRor8>(r);
-        if (g == 0) tile_r[grp] = r;
-        __syncthreads();
-        const uint64_t i = t * 16 + threadIdx.x;
-        if (threadIdx.x < 16 && i < n) st_nt(out + i, tile_r[threadIdx.x]);
-        __syncthreads();
+    for (int c = 0; c < 16; ++c) {
+        const uint64_t o = 4096u * grp + 256u * c + 16u * g;
+        d[c] = o + 16 <= lim ? ld16<true>(reinterpret_cast<const u32x4*>(win + 256u * c)) : u32x4{0, 0, 0, 0};
     }
-}
-
-template <int P, bool NT, bool SPLIT>
-__global__ __launch_bounds__(256) void k_read_ceiling(const uint8_t* __restrict__ pages, uint64_t n,
-                                                     uint64_t* __restrict__ out) {
-    constexpr int G = SPLIT ? P / 4096 : 1;  // groups per page
-    constexpr int PPB = 16 / G;              // pages per tile
-    constexpr int SLICE = P / G;             // bytes per group
-    __shared__ uint64_t tile_r[16];
-    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const uint64_t ntiles = (n + PPB - 1) / PPB;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        const uint64_t pg = t * PPB + grp / G;
-        if (pg < n) {
-            const u32x4* base =
-                reinterpret_cast<const u32x4*>(pages + pg * (uint64_t)P + (uint64_t)SLICE * (grp % G)) + g;
-            uint32_t x = 0, y = 0, z = 0, w = 0;
+    uint32_t x = 0, y = 0, z = 0, v = 0;
 #pragma unroll
-            for (int c = 0; c < SLICE / 256; ++c) {
-                const u32x4 v = ld16<NT>(base + c * 16);
-                x ^= v.x; y += v.y; z ^= v.z; w += v.w;
-            }
-            uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + w);
-            r ^= dpp64<kRowRor1>(r);
-            r ^= dpp64<kRowRor2>(r);
-            r ^= dpp64<kRowRor4>(r);
-            r ^= dpp64<kRowRor8>(r);
-            if (g == 0) tile_r[grp] = r;
-        }
-        __syncthreads();
-        const uint64_t i = t * PPB + threadIdx.x;
-        if (threadIdx.x < PPB && i < n) {
-            uint64_t r = 0;
+    for (int c = 0; c < 16; ++c) {
+        x ^= d[c].x;
+        y += d[c].y;
+        z ^= d[c].z;
+        v += d[c].w;
+    }
+    uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + v);
+    r ^= dpp64<kRowRor1>(r);
+    r ^= dpp64<kRowRor2>(r);
+    r ^= dpp64<kRowRor4>(r);
+    r ^= dpp64<kRowRor8>(r);
+    __shared__ uint64_t part[16];
+    if (g == 0) part[grp] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
 #pragma unroll
-            for (int k = 0; k < G; ++k) r ^= tile_r[threadIdx.x * G + k];
-            st_nt(out + i, r);
-        }
-        __syncthreads();
+        for (int k = 0; k < 16; ++k) t ^= part[k];
+        st_nt(out + w, t);
     }
 }
 
@@ -1585,24 +1291,29 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kTuneKeys = 16;
+// Keys retired in round 2 with the variants they selected (measured slower,
+// DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
+// sort, 12 descriptor slices, 14 XXH64 descriptor sort.  Setting one fails.
+constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false,
+                                      false, false, true,  false, true, false, true, false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
-                                          /*xxh64 nt*/ 0, /*stamp bytes (0 = two-pass)*/ 0, /*xxh64 layout*/ 0,
+                                          /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
                                           /*xxh3 split pages from this size (0 = never)*/ 8192,
-                                          /*descriptor tiles sorted by page size*/ 0,
+                                          /*retired*/ 0,
                                           /*zero-copy page list in kernel arguments*/ 1,
-                                          /*descriptor pages in 4 KiB slices*/ 0,
+                                          /*retired*/ 0,
                                           /*manifest: wide block sums + chain kernel*/ 1,
-                                          /*xxh64 descriptor tiles sorted by page size*/ 0,
+                                          /*retired*/ 0,
                                           /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4};
 }
 int set_tuning(int key, int64_t value) {
-    if (key <= 0 || key >= kTuneKeys || value < 0) return -1;
+    if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
     g_tune[key].store(value, std::memory_order_relaxed);
     return 0;
 }
 int64_t get_tuning(int key) {
-    return (key <= 0 || key >= kTuneKeys) ? -1 : g_tune[key].load(std::memory_order_relaxed);
+    return (key <= 0 || key >= kTuneKeys || kRetired[key]) ? -1 : g_tune[key].load(std::memory_order_relaxed);
 }
 
 namespace {
@@ -1624,22 +1335,20 @@ bool split_pages(uint64_t P) {
     return split > 0 && P >= (uint64_t)split && P >= 8192 && P <= 65536 && (P & (P - 1)) == 0;
 }
 bool rt_batch4() { return g_tune[8].load(std::memory_order_relaxed) != 0; }
-bool use_nt64() { return g_tune[4].load(std::memory_order_relaxed) != 0; }
-bool xxh64_lds_layout() { return g_tune[6].load(std::memory_order_relaxed) != 1; }
 
 // XXH64 LDS kernel launch with the segment depth from PCS_TUNE_XXH64_LAYOUT
-// (0 = default depth, 2/3/4 = depth 1/2/4; 1 is the quad layout, not here).
+// (0 or 1 = default depth, 2/3/4 = depth 1/2/4) and the waves per workgroup
+// from PCS_TUNE_XXH64_WAVES.
 template <int MODE, bool NT, int ADDR>
 void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const uint64_t* off, const uint32_t* len,
                       uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, unsigned long long* fb) {
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
     const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
-    const bool sort = ADDR == kAddrDesc && g_tune[14].load(std::memory_order_relaxed) != 0;
     const int64_t wpb = g_tune[15].load(std::memory_order_relaxed);
-    if (!sort && (wpb == 1 || wpb == 2)) {
+    if (wpb == 1 || wpb == 2) {
         // one workgroup per 16 * wpb pages, every tile covered once
         const unsigned g = (unsigned)std::min<uint64_t>((n + 16 * wpb - 1) / (16 * wpb), 0x7FFFFFFFull);
-#define LW(D, W) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, false, W>), dim3(g), dim3(64 * W), 0, s, base, off, len, P, n, out, ok, fb)
+#define LW(D, W) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, W>), dim3(g), dim3(64 * W), 0, s, base, off, len, P, n, out, ok, fb)
         if (wpb == 1) {
             if (depth == 1) LW(1, 1);
             else if (depth == 2) LW(2, 1);
@@ -1652,18 +1361,10 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
 #undef LW
         return;
     }
-#define L(D, S) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, S>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
-    if constexpr (ADDR == kAddrDesc) {
-        if (sort) {
-            if (depth == 1) L(1, true);
-            else if (depth == 2) L(2, true);
-            else L(4, true);
-            return;
-        }
-    }
-    if (depth == 1) L(1, false);
-    else if (depth == 2) L(2, false);
-    else L(4, false);
+#define L(D) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
+    if (depth == 1) L(1);
+    else if (depth == 2) L(2);
+    else L(4);
 #undef L
 }
 
@@ -1671,8 +1372,7 @@ template <int MODE, bool NT>
 hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
                              unsigned long long* fb, hipStream_t s) {
     const unsigned grid = page_grid(n, kBlock / 16, 1, P);  // kBlock/16 = one 16-page tile per block
-    const int sb = (int)std::min<int64_t>(g_tune[5].load(std::memory_order_relaxed), 256);
-    if (MODE != kStamp && split_pages(P)) {
+    if (split_pages(P)) {
         const uint64_t ppb = 16 / (P / 4096);
         const uint64_t need = (n + ppb - 1) / ppb;
         const unsigned g = (unsigned)std::min<uint64_t>(need, 0x7FFFFFFFull);
@@ -1687,7 +1387,7 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
     switch (P) {
 #define CASE(SZ)                                                                                             \
     case SZ:                                                                                                 \
-        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb, sb); \
+        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb);     \
         break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
@@ -1712,7 +1412,7 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
     const bool aligned16 = ((uintptr_t)pages % 16) == 0;
     const bool aligned8 = ((uintptr_t)pages % 8) == 0;
     if (algo == 0 && aligned16 && P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull) {
-        if (MODE == kStamp && g_tune[5].load(std::memory_order_relaxed) == 0) {
+        if constexpr (MODE == kStamp) {
             // two-pass stamp: digests into a compact array (the fast digest
             // kernel), then one scattered 8-byte write per page
             uint64_t* dig = out;
@@ -1731,14 +1431,14 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
                 e = hipGetLastError();
             }
             return e;
+        } else {
+            return use_nt() ? launch_xxh3_pages<MODE, true>(P, pages, n, out, ok, fb, s)
+                            : launch_xxh3_pages<MODE, false>(P, pages, n, out, ok, fb, s);
         }
-        return use_nt() ? launch_xxh3_pages<MODE, true>(P, pages, n, out, ok, fb, s)
-                        : launch_xxh3_pages<MODE, false>(P, pages, n, out, ok, fb, s);
     }
     if (algo == 1 && aligned8 && P % 8 == 0 && P >= 40 && P <= 0xFFFFFFFFull) {
-        const unsigned grid = page_grid(n, kBlock / 4, 2, P);
         const bool lines = aligned16 && P % 64 == 0 && P >= 128;
-        if (lines && xxh64_lds_layout()) {
+        if (lines) {
             // one workgroup per 64 pages at every page size: the large-page
             // cap of page_grid (8 per CU) cost the LDS kernel 7-8 % on 64 KiB
             // pages (profiles/r01/x64_depth_lab.txt, x64_waves_lab.txt)
@@ -1747,15 +1447,8 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
             else launch_xxh64_lds<MODE, false, kAddrStride>(lgrid, s, pages, nullptr, nullptr, (uint32_t)P, n, out, ok, fb);
             return hipGetLastError();
         }
-        if (lines && use_nt64())
-            hipLaunchKernelGGL((k_xxh64_stride<MODE, true, true>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
-                               n, out, ok, fb);
-        else if (lines)
-            hipLaunchKernelGGL((k_xxh64_stride<MODE, false, true>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
-                               n, out, ok, fb);
-        else
-            hipLaunchKernelGGL((k_xxh64_stride<MODE, false, false>), dim3(grid), dim3(kBlock), 0, s, pages,
-                               (uint32_t)P, n, out, ok, fb);
+        const unsigned grid = page_grid(n, kBlock / 4, 2, P);
+        hipLaunchKernelGGL((k_xxh64_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
         return hipGetLastError();
     }
     return hipErrorNotSupported;  // caller falls back to the descriptor path
@@ -1801,50 +1494,26 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
         // fast kernels for conforming pages, generic lanes for the rest
         if (algo == 0) {
             const unsigned grid = page_grid(n, kBlock / 16, 1);
-            const int dsplit = g_tune[12].load(std::memory_order_relaxed) != 0 ? 1 : 0;
-            if (dsplit) {
-                const unsigned sgrid = (unsigned)std::min<uint64_t>((n + 15) / 16, 0x7FFFFFFFull);
-                if (use_nt())
-                    hipLaunchKernelGGL((k_xxh3_desc_split<MODE, true>), dim3(sgrid), dim3(kBlock), 0, s, base, off, len,
-                                       n, out, ok, fb);
-                else
-                    hipLaunchKernelGGL((k_xxh3_desc_split<MODE, false>), dim3(sgrid), dim3(kBlock), 0, s, base, off,
-                                       len, n, out, ok, fb);
-            }
-#define L(NT_, B4_, SORT_)                                                                                          \
-    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_, SORT_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, \
-                       fb, dsplit)
-            const bool srt = g_tune[10].load(std::memory_order_relaxed) != 0;
+#define L(NT_, B4_) \
+    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
             if (use_nt()) {
-                if (rt_batch4()) {
-                    if (srt) L(true, true, true);
-                    else L(true, true, false);
-                } else {
-                    L(true, false, false);
-                }
+                if (rt_batch4()) L(true, true);
+                else L(true, false);
             } else {
-                if (rt_batch4()) L(false, true, false);
-                else L(false, false, false);
+                if (rt_batch4()) L(false, true);
+                else L(false, false);
             }
 #undef L
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
-            if (xxh64_lds_layout()) {
-                if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
-                else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
-                // pages off the lines shape are left to the quad kernel below
-            }
-            // After the LDS kernel the quad kernel only picks up the pages it
-            // left (usually none): a capped grid-stride pass over the
-            // descriptors instead of one workgroup per 64 pages (14.8 -> ~4 us
-            // on config 3, profiles/r01/desc_passes.txt).
-            const unsigned qgrid = xxh64_lds_layout() ? grid_for(n, kBlock / 4, kBlocksPerCu) : grid;
-            if (use_nt64())
-                hipLaunchKernelGGL((k_xxh64_desc<MODE, true>), dim3(qgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok,
-                                   fb, (int)xxh64_lds_layout());
-            else
-                hipLaunchKernelGGL((k_xxh64_desc<MODE, false>), dim3(qgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok,
-                                   fb, (int)xxh64_lds_layout());
+            if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
+            else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
+            // Pages off the line shape (usually none) go to the quad kernel: a
+            // capped grid-stride pass over the descriptors instead of one
+            // workgroup per 64 pages (14.8 -> ~4 us on config 3,
+            // profiles/r01/desc_passes.txt).
+            const unsigned qgrid = grid_for(n, kBlock / 4, kBlocksPerCu);
+            hipLaunchKernelGGL((k_xxh64_desc<MODE>), dim3(qgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -1983,45 +1652,11 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
     return hipGetLastError();
 }
 
-// Descriptor batches (config 3): k_read_ceiling_desc mirrors k_xxh3_desc's
-// loads — one group per page, 16 pages per block, 4 KiB (16 loads per lane)
-// per step, 256 B steps for the rest — with the hash removed.
-hipError_t run_read_ceiling_desc(const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
-                                 uint64_t* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const unsigned grid = page_grid(n, kBlock / 16, 1);
-    if (use_nt()) hipLaunchKernelGGL((k_read_ceiling_desc<true>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out);
-    else hipLaunchKernelGGL((k_read_ceiling_desc<false>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out);
-    return hipGetLastError();
-}
-
-hipError_t run_read_ceiling(const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const bool nt = use_nt();
-    if (split_pages(P)) {  // mirror k_xxh3_split's tiles
-        const unsigned grid = (unsigned)std::min<uint64_t>((n + 16 / (P / 4096) - 1) / (16 / (P / 4096)), 0x7FFFFFFFull);
-        switch (P) {
-#define CASE(SZ)                                                                                                  \
-    case SZ:                                                                                                      \
-        if (nt) hipLaunchKernelGGL((k_read_ceiling<SZ, true, true>), dim3(grid), dim3(kBlock), 0, s, pages, n, out);  \
-        else hipLaunchKernelGGL((k_read_ceiling<SZ, false, true>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); \
-        break;
-            CASE(8192) CASE(16384) CASE(32768) CASE(65536)
-#undef CASE
-        }
-        return hipGetLastError();
-    }
-    const unsigned grid = page_grid(n, kBlock / 16, 1);
-    switch (P) {
-#define CASE(SZ)                                                                                                   \
-    case SZ:                                                                                                       \
-        if (nt) hipLaunchKernelGGL((k_read_ceiling<SZ, true, false>), dim3(grid), dim3(kBlock), 0, s, pages, n, out);  \
-        else hipLaunchKernelGGL((k_read_ceiling<SZ, false, false>), dim3(grid), dim3(kBlock), 0, s, pages, n, out); \
-        break;
-        CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
-#undef CASE
-        default: return hipErrorNotSupported;
-    }
+hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s) {
+    if (bytes < 16) return hipSuccess;
+    const uint64_t nwin = (bytes + kStreamWin - 1) / kStreamWin;
+    if (nwin > 0x7FFFFFFFull) return hipErrorNotSupported;
+    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)nwin), dim3(kBlock), 0, s, buf, bytes & ~uint64_t(15), out);
     return hipGetLastError();
 }
 

@@ -209,18 +209,9 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_XXH64_BLOCKS_PER_CU  [0] same for XXH64 (one block per 64 pages)
  *   PCS_TUNE_NT_LOADS             [1] XXH3 page loads non-temporal (1) or
  *                                     default cache policy (0)
- *   PCS_TUNE_XXH64_NT_LOADS       [0] same for the XXH64 page kernels (their
- *                                     64-byte-per-page pieces lose the line's
- *                                     other half under nt: measured slower)
- *   PCS_TUNE_STAMP_BYTES          [0] bytes of each page a fixed-size XXH3
- *                                     stamp rewrites (8, 64, 128 or 256): the
- *                                     digest plus the unchanged bytes after it;
- *                                     0 = two passes (digest kernel into a
- *                                     compact array, then a scatter pass)
- *   PCS_TUNE_XXH64_LAYOUT         [0] 0 = 16-lane 256 B loads with an LDS hand-
- *                                     off to the hashing quads (uses
- *                                     PCS_TUNE_NT_LOADS); 1 = each quad loads
- *                                     its own 64 B pieces
+ *   PCS_TUNE_XXH64_LAYOUT         [0] segments in flight per XXH64 LDS-kernel
+ *                                     step: 0 or 1 = default (2), 2 -> 1,
+ *                                     3 -> 2, 4 -> 4
  *   PCS_TUNE_ZERO_COPY            [1] host batches over registered pages:
  *                                     1 = zero-copy (one launch, pages read in
  *                                     place); 0 = stage through device memory
@@ -235,39 +226,28 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     split over P/4096 groups, one 4 KiB slice
  *                                     each, with the scramble chain run from
  *                                     block sums in LDS; 0 = never
- *   PCS_TUNE_DESC_SORT            [0] XXH3 descriptor batches (nt loads, 4-block
- *                                     batches): 1 = hand each tile's 16 pages
- *                                     to the groups in order of size
  *   PCS_TUNE_INLINE_LIST          [1] zero-copy XXH3 batches of <= 256 pages
  *                                     pass the page list in the kernel
  *                                     arguments (0 = read it from host memory)
- *   PCS_TUNE_DESC_SPLIT           [0] 1 = XXH3 descriptor pages of 4, 8, 12 or
- *                                     16 KiB are hashed in 4 KiB slices dealt
- *                                     to the groups round by round; 0 = one
- *                                     group walks each page (measured faster)
  *   PCS_TUNE_MANIFEST_WIDE        [1] manifests at 8-byte alignment: block
  *                                     sums over the whole GPU, then one chain
  *                                     per chunk (0 = one workgroup per chunk)
- *   PCS_TUNE_XXH64_DESC_SORT      [0] XXH64 descriptor batches: 1 = hand
- *                                     each 64-page tile to the four waves in
- *                                     order of page size (measured slower)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
- *                                     kernel (1, 2 or 4; 16 pages per wave) */
+ *                                     kernel (1, 2 or 4; 16 pages per wave)
+ * Keys 4, 5, 10, 12 and 14 selected variants that measured slower (XXH64 quad
+ * nt loads, in-place stamp widths, descriptor tile sorts and 4 KiB slices);
+ * they were retired in round 2: setting one fails and reading
+ * one returns -1. */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
     PCS_TUNE_NT_LOADS = 3,
-    PCS_TUNE_XXH64_NT_LOADS = 4,
-    PCS_TUNE_STAMP_BYTES = 5,
     PCS_TUNE_XXH64_LAYOUT = 6,
     PCS_TUNE_ZERO_COPY = 7,
     PCS_TUNE_XXH3_RT_BATCH = 8,
     PCS_TUNE_XXH3_SPLIT_PAGES = 9,
-    PCS_TUNE_DESC_SORT = 10,
     PCS_TUNE_INLINE_LIST = 11,
-    PCS_TUNE_DESC_SPLIT = 12,
     PCS_TUNE_MANIFEST_WIDE = 13,
-    PCS_TUNE_XXH64_DESC_SORT = 14,
     PCS_TUNE_XXH64_WAVES = 15,
 };
 int pcs_set_tuning(int key, int64_t value);
@@ -292,16 +272,14 @@ int pcs_gen_desc_dev(void *d_base, const uint64_t *d_off, const uint32_t *d_len,
 /* XOR 0xFF into byte `byte_offset` of every `every`-th page (pages 0, every, ...). */
 int pcs_flip_byte_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, uint64_t every,
                       uint64_t byte_offset, pcs_stream_t stream);
-/* Streaming-read ceiling: same load pattern as the XXH3 page kernel with the
- * hash replaced by an xor/add fold (page_size a power of two, 256..65536;
- * split slices for the page sizes PCS_TUNE_XXH3_SPLIT_PAGES selects). */
-int pcs_read_ceiling_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages,
-                         uint64_t *d_out, pcs_stream_t stream);
-/* The same for descriptor batches: the XXH3 descriptor kernel's loads (one
- * 16-lane group per page, 4 KiB per step) over pages with len % 256 == 0 at
- * 16-byte-aligned offsets (others are skipped, their result is 0). */
-int pcs_read_ceiling_desc_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
-                              uint64_t n, uint64_t *d_out, pcs_stream_t stream);
+/* Streaming-read ceiling: a plain read of [d_buf, d_buf + bytes) (16-byte
+ * aligned; a trailing partial 16 bytes is ignored) with the fastest read
+ * pattern measured (64 KiB windows per workgroup, XCD-contiguous order, nt
+ * dwordx4 loads), folded into one word per 64 KiB window:
+ * d_out[0 .. ceil(bytes / 65536)).  The roofline's measured companion: the
+ * hash kernels are compared with the rate at which the same bytes can merely
+ * be read. */
+int pcs_stream_read_dev(const void *d_buf, uint64_t bytes, uint64_t *d_out, pcs_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -116,7 +116,7 @@ def test_counters_and_tuning_defaults():
     assert pcs.counter(pcs.COUNTER_ZERO_COPY_LAUNCHES) >= 0
     assert pcs.lib().pcs_counter(99) == 0
     assert pcs.get_tuning(pcs.TUNE_ZERO_COPY) == 1
-    assert pcs.get_tuning(pcs.TUNE_STAMP_BYTES) == 0
+    assert pcs.get_tuning(5) == -1  # retired (in-place stamp width)
     assert pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES) == 8192
     assert pcs.get_tuning(pcs.TUNE_INLINE_LIST) == 1
 

@@ -185,12 +185,11 @@ def test_desc_odd_shapes(algo):
     assert okh[lens < 8].sum() == 0  # header-less pages never validate
 
 
-@pytest.mark.parametrize("dsplit", [0, 1])
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
-def test_desc_mixed_wide(algo, dsplit):
+def test_desc_mixed_wide(algo):
     """Many pages of many sizes in random order: every kernel split of the
-    descriptor path (4 KiB-slice tiles, run-time-size groups, generic lanes)
-    sees neighbours of other shapes."""
+    descriptor path (run-time-size groups, XXH64 LDS and quad kernels, generic
+    lanes) sees neighbours of other shapes."""
     rng = np.random.default_rng(0xD35C)
     sizes = np.array([4096, 8192, 12288, 16384, 20480, 32768, 5120, 1280, 256, 4104, 65536, 100], dtype=np.uint32)
     n = 3000
@@ -208,12 +207,7 @@ def test_desc_mixed_wide(algo, dsplit):
     d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
     want = np.array([oracle.pages_digest(host[int(o):int(o) + int(L)], int(L), algo)[0] for o, L in zip(offs, lens)],
                     dtype=np.uint64)
-    saved = pcs.get_tuning(pcs.TUNE_DESC_SPLIT)
-    pcs.set_tuning(pcs.TUNE_DESC_SPLIT, dsplit)
-    try:
-        _desc_mixed_wide_checks(base, d_off, d_len, n, algo, offs, lens, want)
-    finally:
-        pcs.set_tuning(pcs.TUNE_DESC_SPLIT, saved)
+    _desc_mixed_wide_checks(base, d_off, d_len, n, algo, offs, lens, want)
 
 
 def _desc_mixed_wide_checks(base, d_off, d_len, n, algo, offs, lens, want):
@@ -429,48 +423,34 @@ def test_full_size_64k_chunks_sampled():
     torch.cuda.empty_cache()
 
 
-def _ceiling_fold(pages: np.ndarray, P: int) -> np.ndarray:
-    """What pcs_read_ceiling_dev computes: per lane (16 per slice) xor/add folds
-    of its 16-byte pieces, xor-reduced over lanes and slices."""
-    G = P // 4096 if P >= pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES) > 0 else 1
-    w = pages.view(np.uint32).reshape(-1, G, P // G // 256, 16, 4)
+def _stream_fold(buf: np.ndarray) -> np.ndarray:
+    """What pcs_stream_read_dev computes per 64 KiB window: lane (group k,
+    lane g) folds its 16 pieces (bytes 4096k + 256c + 16g) with xor/add, lanes
+    and groups xor-reduced; a partial window reads only its whole 16 B pieces."""
+    nbytes = buf.nbytes - buf.nbytes % 16
+    nwin = (nbytes + 65535) // 65536
+    pad = np.zeros(nwin * 65536, dtype=np.uint8)
+    pad[:nbytes] = buf[:nbytes]
+    w = pad.view(np.uint32).reshape(nwin, 16, 16, 16, 4)  # window, group, chunk c, lane g, word
     x = np.bitwise_xor.reduce(w[..., 0], axis=2).astype(np.uint64)
     y = w[..., 1].astype(np.uint64).sum(axis=2) & 0xFFFFFFFF
     z = np.bitwise_xor.reduce(w[..., 2], axis=2).astype(np.uint64)
     ww = w[..., 3].astype(np.uint64).sum(axis=2) & 0xFFFFFFFF
     r = ((x ^ z) << np.uint64(32)) | ((y + ww) & np.uint64(0xFFFFFFFF))
-    return np.bitwise_xor.reduce(r.reshape(r.shape[0], -1), axis=1)
+    return np.bitwise_xor.reduce(r.reshape(nwin, -1), axis=1)
 
 
-@pytest.mark.parametrize("P", [4096, 8192, 65536])
-def test_read_ceiling_fold(P):
-    """The roofline's read-ceiling kernel reads every byte of the layout it mirrors."""
-    n = 1000 if P <= 8192 else 70
-    buf = dev_pages(P, n, 3, 0)
-    out = torch.empty(n, dtype=torch.int64, device=DEV)
-    pcs.read_ceiling(buf, P, n, out)
-    assert np.array_equal(u64(out), _ceiling_fold(buf.cpu().numpy(), P))
-
-
-def test_read_ceiling_desc_fold():
-    """The config-3 read ceiling (descriptor layout) reads every byte of every
-    page: one 16-lane group per page, no slices."""
-    n = 700
-    offs, lens, total = mixed_layout(0x5EED0003, 0, n)
-    base = torch.empty(total, dtype=torch.uint8, device=DEV)
-    d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
-    d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
-    pcs.gen_desc(base, d_off, d_len, n, 0x5EED0003, 0)
-    out = torch.empty(n, dtype=torch.int64, device=DEV)
-    pcs.read_ceiling_desc(base, d_off, d_len, n, out)
-    host = base.cpu().numpy()
-    saved = pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES)
-    pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, 0)  # the fold helper then folds whole pages
-    try:
-        want = np.array([_ceiling_fold(host[o:o + l], int(l))[0] for o, l in zip(offs, lens)], dtype=np.uint64)
-    finally:
-        pcs.set_tuning(pcs.TUNE_XXH3_SPLIT_PAGES, saved)
-    assert np.array_equal(u64(out), want)
+@pytest.mark.parametrize("nbytes", [16, 4096, 65536, 65536 * 7, 65536 * 300 + 4096 + 48, 65536 * 5 + 23])
+def test_stream_read_fold(nbytes):
+    """The read-ceiling kernel reads every (whole 16-byte piece of every) byte
+    of the range exactly once, full and partial windows alike."""
+    host = np.random.default_rng(nbytes).integers(0, 256, size=nbytes, dtype=np.uint8)
+    buf = torch.from_numpy(host).to(DEV)
+    nwin = (nbytes - nbytes % 16 + 65535) // 65536
+    out = torch.zeros(nwin + 1, dtype=torch.int64, device=DEV)
+    pcs.stream_read(buf, nbytes, out)
+    got = u64(out)
+    assert np.array_equal(got[:nwin], _stream_fold(host)) and got[nwin] == 0
 
 
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])

@@ -17,6 +17,6 @@ out = torch.empty(n, dtype=torch.int64, device="cuda:0")
 for _ in range(3):
     pcs.pages_digest(pages, P, n, pcs.XXH3_64, out=out)
     pcs.pages_digest(pages, P, n, pcs.XXH64, out=out)
-    pcs.read_ceiling(pages, P, n, out)
+    pcs.stream_read(pages, n * P, out)
 torch.cuda.synchronize()
 print("ok")

@@ -481,9 +481,8 @@ int main(int argc, char** argv) {
     add("batchstore M=1 nt-store", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_batchstore<4096, 1, true>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
     add("group16 nt xcd-contiguous tiles", [=](hipStream_t st) { hipLaunchKernelGGL((k_group16_xcd<4096>), dim3(n / 16), dim3(256), 0, st, pages, n, out); });
     add("PRODUCT pcs_pages_validate_dev xxh3", [=](hipStream_t st) { pcs_pages_validate_dev(pages, 4096, n, 0, reinterpret_cast<uint8_t*>(out), out + n / 2, (pcs_stream_t)st); });
-    for (int sbytes : {0, 8, 64})
-        add("PRODUCT pcs_pages_stamp_dev xxh3 w=" + std::to_string(sbytes), [=](hipStream_t st) { pcs_set_tuning(PCS_TUNE_STAMP_BYTES, sbytes); pcs_pages_stamp_dev(pages, 4096, n, 0, (pcs_stream_t)st); });
-    add("PRODUCT pcs_read_ceiling_dev", [=](hipStream_t st) { pcs_read_ceiling_dev(pages, 4096, n, out, (pcs_stream_t)st); });
+    add("PRODUCT pcs_pages_stamp_dev xxh3", [=](hipStream_t st) { pcs_pages_stamp_dev(pages, 4096, n, 0, (pcs_stream_t)st); });
+    add("PRODUCT pcs_stream_read_dev", [=](hipStream_t st) { pcs_stream_read_dev(pages, 4096 * n, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh3", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 0, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh64", [=](hipStream_t st) { pcs_pages_digest_dev(pages, 4096, n, 1, out, (pcs_stream_t)st); });
     for (int bpc : {2, 4}) {
@@ -548,7 +547,7 @@ static int main_big(int rounds) {
         add("wg-per-page nt bpc=" + std::to_string(bpc), bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_wg_page64k<true>), dim3(cus * bpc), dim3(256), 0, st, pages, n, out); });
     add("wg-per-page nt nonpersistent", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_wg_page64k<true>), dim3(n), dim3(256), 0, st, pages, n, out); });
     add("wg-per-page plain nonpersistent", bytes, [=](hipStream_t st) { hipLaunchKernelGGL((k_wg_page64k<false>), dim3(n), dim3(256), 0, st, pages, n, out); });
-    add("PRODUCT pcs_read_ceiling_dev 64K", bytes, [=](hipStream_t st) { pcs_read_ceiling_dev(pages, P, n, out, (pcs_stream_t)st); });
+    add("PRODUCT pcs_stream_read_dev 64K", bytes, [=](hipStream_t st) { pcs_stream_read_dev(pages, P * n, out, (pcs_stream_t)st); });
     add("PRODUCT pcs_pages_digest_dev xxh3 64K", bytes, [=](hipStream_t st) { pcs_pages_digest_dev(pages, P, n, 0, out, (pcs_stream_t)st); });
     hipEvent_t a, b;
     CK(hipEventCreate(&a));

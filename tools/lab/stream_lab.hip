@@ -1,0 +1,245 @@
+// stream_lab.hip — how fast can MI355X stream-read a device buffer?  (not
+// part of the product; VERDICT r01 asked for a real read ceiling).
+//
+// Pure reads, no hash: one-shot workgroups, each owning a contiguous window,
+// windows renumbered so the blocks of one XCD walk one contiguous eighth of
+// the buffer (xcd_tile, cdna_hip_programming.md T1).  Variants: window size,
+// workgroup size, nt vs default loads, lane layout (1 KiB contiguous per
+// wave-instruction vs the product's 16-lane groups over 4 KiB slices), and
+// loads in flight per lane.  Compared in interleaved rounds against the
+// product's XXH3 kernels on 4 KiB pages (config 2/5) and mixed pages
+// (config 3), over 4 GiB, 9.33 GiB and 32 GiB.
+//
+//   ./tools/lab/stream_lab [rounds]
+#include <hip/hip_runtime.h>
+
+#include "eloqstore_pcs.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                                           \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess) {                                                                         \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));     \
+            std::exit(1);                                                                               \
+        }                                                                                               \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t nb) {
+    const uint64_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// LAYOUT 0: instruction i of the workgroup covers bytes [i*T*16, (i+1)*T*16)
+//           of its window (each wave-instruction = 1 KiB contiguous).
+// LAYOUT 1: the product's 16-lane groups: group k of the workgroup owns the
+//           4 KiB slices k, k + T/16, ... of the window; lane g reads 16 B at
+//           256c + 16g of a slice (a wave-instruction = 4 x 256 B segments).
+template <int CH, int T, bool NT, bool XCD, int LAYOUT>
+__global__ __launch_bounds__(T) void k_win(const uint8_t* __restrict__ buf, uint64_t nwin, uint64_t* out) {
+    constexpr int L = CH / (T * 16);  // loads per lane
+    const uint64_t w = XCD ? xcd_tile(blockIdx.x, nwin) : blockIdx.x;
+    const u32x4* base = reinterpret_cast<const u32x4*>(buf + w * (uint64_t)CH);
+    u32x4 d[L];
+    if constexpr (LAYOUT == 0) {
+#pragma unroll
+        for (int i = 0; i < L; ++i) d[i] = ld<NT>(base + i * T + threadIdx.x);
+    } else {
+        const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+        constexpr int G = T / 16;
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            const int slice = grp + (i / 16) * G, c = i % 16;
+            d[i] = ld<NT>(base + slice * 256 + c * 16 + g);
+        }
+    }
+    uint32_t x = 0, y = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        x ^= d[i].x ^ d[i].z;
+        y += d[i].y + d[i].w;
+    }
+    if ((x ^ y) == 0x9E3779B9u) out[w] = x;  // practically never: keeps the loads live
+}
+
+// The same with dynamic LDS reserved only to cap workgroups per CU (160 KiB
+// of LDS per CU / the reservation), i.e. bytes in flight per CU.
+template <int CH, int T, int LAYOUT>
+__global__ __launch_bounds__(T) void k_win_occ(const uint8_t* __restrict__ buf, uint64_t nwin, uint64_t* out) {
+    extern __shared__ uint32_t pad[];
+    constexpr int L = CH / (T * 16);
+    const uint64_t w = xcd_tile(blockIdx.x, nwin);
+    const u32x4* base = reinterpret_cast<const u32x4*>(buf + w * (uint64_t)CH);
+    u32x4 d[L];
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    constexpr int G = T / 16;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        if constexpr (LAYOUT == 0) d[i] = ld<true>(base + i * T + threadIdx.x);
+        else d[i] = ld<true>(base + (grp + (i / 16) * G) * 256 + (i % 16) * 16 + g);
+    }
+    uint32_t x = 0, y = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        x ^= d[i].x ^ d[i].z;
+        y += d[i].y + d[i].w;
+    }
+    if ((x ^ y) == 0x9E3779B9u) {
+        pad[threadIdx.x] = x;
+        out[w] = pad[(threadIdx.x + 1) % T];
+    }
+}
+
+__global__ void k_fill(uint64_t* p, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = i * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+__global__ void k_spin(long long cycles) {
+    const long long t0 = clock64();
+    while (clock64() - t0 < cycles) {
+    }
+}
+
+// Config 3's size rule (tests/workload.py mixed_sizes): class = mix((seed ^ p)
+// + (0x5A5A5A5A + 1) * golden) % 3 -> 4/8/16 KiB, packed.
+static uint64_t mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct V {
+    std::string name;
+    double bytes;
+    std::function<void(hipStream_t)> run;
+    std::vector<float> ms;
+};
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? std::atoi(argv[1]) : 9;
+    const uint64_t big = 32ull << 30;
+    uint8_t* buf;
+    uint64_t* out;
+    CK(hipMalloc(&buf, big));
+    CK(hipMalloc(&out, 64ull << 20));
+    hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(buf), big / 8);
+    CK(hipDeviceSynchronize());
+
+    // config 3 descriptors over the first 9.33 GiB
+    const uint64_t n3 = 1 << 20;
+    std::vector<uint64_t> off(n3);
+    std::vector<uint32_t> len(n3);
+    uint64_t o = 0;
+    for (uint64_t p = 0; p < n3; ++p) {
+        const uint64_t cls = mix((0x5EED0003ull ^ p) + (0x5A5A5A5Aull + 1) * 0x9E3779B97F4A7C15ull) % 3;
+        len[p] = 4096u << cls;
+        off[p] = o;
+        o += len[p];
+    }
+    const uint64_t bytes3 = o;
+    uint64_t* d_off;
+    uint32_t* d_len;
+    CK(hipMalloc(&d_off, n3 * 8));
+    CK(hipMalloc(&d_len, n3 * 4));
+    CK(hipMemcpy(d_off, off.data(), n3 * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_len, len.data(), n3 * 4, hipMemcpyHostToDevice));
+    if (pcs_gen_desc_dev(buf, d_off, d_len, n3, 0x5EED0003, 0, nullptr)) return 2;
+
+    std::vector<V> vs;
+    auto add_win = [&](const char* tag, uint64_t bytes, auto kern, int ch, int t) {
+        const uint64_t nwin = bytes / ch;
+        vs.push_back({std::string(tag), (double)(nwin * ch), [=](hipStream_t s) {
+                          hipLaunchKernelGGL(kern, dim3((unsigned)nwin), dim3(t), 0, s, buf, nwin, out);
+                      }, {}});
+    };
+    const bool only_product = argc > 2 && std::string(argv[2]) == "product";
+    for (uint64_t bytes : {uint64_t(4) << 30, bytes3 & ~((uint64_t(128) << 10) - 1), big}) {
+        if (only_product) break;
+        char t[128];
+        auto nm = [&](const char* v) {
+            std::snprintf(t, sizeof t, "%-34s %6.2f GiB", v, bytes / double(1ull << 30));
+            return t;
+        };
+        add_win(nm("win64K T256 nt xcd L0"), bytes, k_win<65536, 256, true, true, 0>, 65536, 256);
+        add_win(nm("win64K T256 nt xcd L1(groups)"), bytes, k_win<65536, 256, true, true, 1>, 65536, 256);
+        add_win(nm("win64K T256 nt noxcd L0"), bytes, k_win<65536, 256, true, false, 0>, 65536, 256);
+        add_win(nm("win64K T256 plain xcd L0"), bytes, k_win<65536, 256, false, true, 0>, 65536, 256);
+        add_win(nm("win32K T256 nt xcd L0"), bytes, k_win<32768, 256, true, true, 0>, 32768, 256);
+        add_win(nm("win128K T256 nt xcd L0 (32/lane)"), bytes, k_win<131072, 256, true, true, 0>, 131072, 256);
+        add_win(nm("win128K T512 nt xcd L0"), bytes, k_win<131072, 512, true, true, 0>, 131072, 512);
+        add_win(nm("win64K T512 nt xcd L0 (8/lane)"), bytes, k_win<65536, 512, true, true, 0>, 65536, 512);
+        add_win(nm("win128K T1024 nt xcd L0"), bytes, k_win<131072, 1024, true, true, 0>, 131072, 1024);
+        for (int wpc : {2, 3, 4, 5, 6, 8}) {
+            const uint64_t nwin = bytes / 65536;
+            const unsigned lds = (160u * 1024u) / wpc - 1024;
+            char nmb[64];
+            std::snprintf(nmb, sizeof nmb, "win64K groups occ %d WG/CU", wpc);
+            vs.push_back({std::string(nm(nmb)), (double)(nwin * 65536), [=](hipStream_t s) {
+                              hipLaunchKernelGGL((k_win_occ<65536, 256, 1>), dim3((unsigned)nwin), dim3(256), lds, s, buf,
+                                                 nwin, out);
+                          }, {}});
+        }
+    }
+    vs.push_back({"PRODUCT digest 4K pages 4 GiB (config 2)", double(4ull << 30), [=](hipStream_t s) {
+                      pcs_pages_digest_dev(buf, 4096, 1 << 20, PCS_XXH3_64, out, (pcs_stream_t)s);
+                  }, {}});
+    vs.push_back({"PRODUCT digest 4K pages 32 GiB (config 5)", double(big), [=](hipStream_t s) {
+                      pcs_pages_digest_dev(buf, 4096, 1 << 23, PCS_XXH3_64, out, (pcs_stream_t)s);
+                  }, {}});
+    vs.push_back({"PRODUCT desc digest config 3 xxh3", double(bytes3), [=](hipStream_t s) {
+                      pcs_desc_digest_dev(buf, d_off, d_len, n3, PCS_XXH3_64, out, (pcs_stream_t)s);
+                  }, {}});
+    vs.push_back({"PRODUCT desc digest config 3 xxh64", double(bytes3), [=](hipStream_t s) {
+                      pcs_desc_digest_dev(buf, d_off, d_len, n3, PCS_XXH64, out, (pcs_stream_t)s);
+                  }, {}});
+    vs.push_back({"PRODUCT stream_read config 3 arena", double(bytes3 & ~uint64_t(15)), [=](hipStream_t s) {
+                      pcs_stream_read_dev(buf, bytes3, out, (pcs_stream_t)s);
+                  }, {}});
+
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (auto& v : vs) v.run(s);
+    CK(hipStreamSynchronize(s));
+    CK(hipGetLastError());
+    for (int r = 0; r < rounds; ++r)
+        for (auto& v : vs) {
+            hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 100000LL);
+            CK(hipEventRecord(a, s));
+            v.run(s);
+            CK(hipEventRecord(b, s));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.ms.push_back(ms);
+        }
+    CK(hipGetLastError());
+    std::printf("%-58s %9s %9s %9s\n", "variant", "med_ms", "GB/s", "best");
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const double med = v.ms[v.ms.size() / 2], best = v.ms.front();
+        std::printf("%-58s %9.4f %9.1f %9.1f\n", v.name.c_str(), med, v.bytes / med / 1e6, v.bytes / best / 1e6);
+    }
+    return 0;
+}
