@@ -6,6 +6,7 @@
 // All compute is on the GPU; there is no CPU hashing in this library.
 #include "eloqstore_pcs.h"
 #include "eloqstore_pcs_internal.h"
+#include "region_registry.h"
 
 #include <hip/hip_runtime.h>
 
@@ -93,48 +94,23 @@ int desc_common(int mode, const void* d_base, const uint64_t* d_off, const uint3
 // ---------------------------------------------------------------------------
 // registered host regions (zero-copy page pools)
 // ---------------------------------------------------------------------------
-struct Region {
-    uint64_t bytes;
-    uintptr_t dev;  // device-visible address of the region base
-    bool allocated; // pcs_host_alloc_pinned (freed there, not unregistered)
-};
-std::shared_mutex g_reg_mu;
-std::map<uintptr_t, Region> g_regions;  // keyed by host base address
+pcs::RegionRegistry g_regions;
 
 int add_region(void* p, uint64_t bytes, bool allocated) {
     void* dev = nullptr;
     const hipError_t e = hipHostGetDevicePointer(&dev, p, 0);
     if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
-    std::unique_lock lk(g_reg_mu);
-    const uintptr_t b = reinterpret_cast<uintptr_t>(p);
-    auto it = g_regions.upper_bound(b);
-    if (it != g_regions.end() && it->first < b + bytes) return fail(PCS_ERR_INVALID, "region overlaps a registered one");
-    if (it != g_regions.begin()) {
-        auto pv = std::prev(it);
-        if (pv->first + pv->second.bytes > b) return fail(PCS_ERR_INVALID, "region overlaps a registered one");
+    switch (g_regions.add(reinterpret_cast<uintptr_t>(p), bytes, reinterpret_cast<uintptr_t>(dev), allocated)) {
+        case pcs::RegionRegistry::kOk: return PCS_OK;
+        case pcs::RegionRegistry::kOverlap: return fail(PCS_ERR_INVALID, "region overlaps a registered one");
+        default: return fail(PCS_ERR_INVALID, "region wraps the address space");
     }
-    g_regions.emplace(b, Region{bytes, reinterpret_cast<uintptr_t>(dev), allocated});
-    return PCS_OK;
 }
 
 // Device-visible addresses of pages[0..n) when every page [p, p + P) lies in a
 // registered region and is 16-byte aligned; false otherwise.
 bool translate_registered(const void* const* pages, uint64_t n, uint64_t P, uint64_t* dev_out) {
-    std::shared_lock lk(g_reg_mu);
-    if (g_regions.empty()) return false;
-    auto hint = g_regions.end();
-    for (uint64_t i = 0; i < n; ++i) {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(pages[i]);
-        if (a % 16) return false;
-        if (hint == g_regions.end() || a < hint->first || a + P > hint->first + hint->second.bytes) {
-            auto it = g_regions.upper_bound(a);
-            if (it == g_regions.begin()) return false;
-            hint = std::prev(it);
-            if (a + P > hint->first + hint->second.bytes) return false;
-        }
-        dev_out[i] = hint->second.dev + (a - hint->first);
-    }
-    return true;
+    return g_regions.translate(pages, n, P, dev_out);
 }
 
 template <typename T>
@@ -249,16 +225,12 @@ bool contiguous_pinned(const void* const* pages, uint64_t n, uint64_t P) {
     for (uint64_t i = 1; i < n; ++i)
         if (pages[i] != base + i * P) return false;
     const uint8_t* last = base + n * P - 1;
-    {
-        // Regions this library registered or allocated have known extents
-        // (hipMemGetAddressRange does not resolve hipHostRegister'ed memory).
-        std::shared_lock lk(g_reg_mu);
-        const uintptr_t a = reinterpret_cast<uintptr_t>(base);
-        auto it = g_regions.upper_bound(a);
-        if (it != g_regions.begin()) {
-            const auto& [rb, r] = *std::prev(it);
-            if (a < rb + r.bytes) return reinterpret_cast<uintptr_t>(last) < rb + r.bytes;
-        }
+    // Regions this library registered or allocated have known extents
+    // (hipMemGetAddressRange does not resolve hipHostRegister'ed memory).
+    switch (g_regions.run(reinterpret_cast<uintptr_t>(base), reinterpret_cast<uintptr_t>(last))) {
+        case pcs::RegionRegistry::kInside: return true;
+        case pcs::RegionRegistry::kPastEnd: return false;
+        case pcs::RegionRegistry::kNotRegistered: break;
     }
     auto pinned_alloc = [](const uint8_t* p, uintptr_t* alloc_base, size_t* alloc_size) {
         hipPointerAttribute_t attr{};
@@ -648,27 +620,18 @@ int pcs_host_alloc_pinned(uint64_t bytes, void** out) {
 
 int pcs_host_free_pinned(void* p) {
     if (!p) return PCS_OK;
-    {
-        std::unique_lock lk(g_reg_mu);
-        auto it = g_regions.find(reinterpret_cast<uintptr_t>(p));
-        if (it == g_regions.end() || !it->second.allocated)
-            return fail(PCS_ERR_INVALID, "not a pcs_host_alloc_pinned allocation");
-        g_regions.erase(it);
-    }
+    if (g_regions.remove(reinterpret_cast<uintptr_t>(p), true) != pcs::RegionRegistry::kOk)
+        return fail(PCS_ERR_INVALID, "not a pcs_host_alloc_pinned allocation");
     return finish(hipHostFree(p), "hipHostFree");
 }
 
 int pcs_host_register(void* p, uint64_t bytes) {
     if (!p || bytes == 0) return fail(PCS_ERR_INVALID, "null pointer or zero size");
     if (int rc = require_device()) return rc;
-    {
-        std::shared_lock lk(g_reg_mu);  // reject overlaps before pinning anything
-        const uintptr_t b = reinterpret_cast<uintptr_t>(p);
-        auto it = g_regions.upper_bound(b);
-        if ((it != g_regions.end() && it->first < b + bytes) ||
-            (it != g_regions.begin() && std::prev(it)->first + std::prev(it)->second.bytes > b))
-            return fail(PCS_ERR_INVALID, "region overlaps a registered one");
-    }
+    const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+    if (!pcs::RegionRegistry::valid_range(b, bytes)) return fail(PCS_ERR_INVALID, "region wraps the address space");
+    if (g_regions.overlaps(b, bytes))  // reject overlaps before pinning anything
+        return fail(PCS_ERR_INVALID, "region overlaps a registered one");
     hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
     if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
     if (int rc = add_region(p, bytes, false)) {
@@ -680,13 +643,8 @@ int pcs_host_register(void* p, uint64_t bytes) {
 
 int pcs_host_unregister(void* p) {
     if (!p) return fail(PCS_ERR_INVALID, "null pointer");
-    {
-        std::unique_lock lk(g_reg_mu);
-        auto it = g_regions.find(reinterpret_cast<uintptr_t>(p));
-        if (it == g_regions.end() || it->second.allocated)
-            return fail(PCS_ERR_INVALID, "not the base of a pcs_host_register region");
-        g_regions.erase(it);
-    }
+    if (g_regions.remove(reinterpret_cast<uintptr_t>(p), false) != pcs::RegionRegistry::kOk)
+        return fail(PCS_ERR_INVALID, "not the base of a pcs_host_register region");
     return finish(hipHostUnregister(p), "hipHostUnregister");
 }
 
