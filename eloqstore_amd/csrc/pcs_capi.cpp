@@ -328,6 +328,7 @@ int check_host_batch_args(const void* const* pages, uint64_t P, uint64_t n, int 
     if (!valid_algo(algo)) return fail(PCS_ERR_INVALID, "algo must be PCS_XXH3_64 or PCS_XXH64");
     if (P < 8 || P > 0xFFFFFFFFull) return fail(PCS_ERR_INVALID, "page_size must be in [8, 2^32)");
     if (n && !pages) return fail(PCS_ERR_INVALID, "pages is null");
+    if (n > UINT64_MAX / P) return fail(PCS_ERR_INVALID, "n_pages * page_size overflows 64 bits");
     for (uint64_t i = 0; i < n; ++i)
         if (!pages[i]) return fail(PCS_ERR_INVALID, "null page pointer in batch");
     return PCS_OK;

@@ -1,0 +1,60 @@
+"""Sanitizer builds of the host code (the reference's WITH_ASAN,
+CMakeLists.txt:19-44), run on the CPU:
+
+- tests/cpp/host_logic_test_{asan,tsan}: the zero-copy page-pool registry
+  (eloqstore_amd/csrc/region_registry.h) under ASAN+UBSan and under TSan,
+  including concurrent register / unregister / translate threads;
+- tests/cpp/capi_sanitize_test: pcs_capi.cpp + page_checksum.cpp built with
+  ASAN+UBSan and driven with no GPU: every compute entry point fails with
+  PCS_ERR_NO_DEVICE, argument checks, shard ranges at the uint64 edge, the
+  skip_verify path, per-thread last-error strings.
+
+`make -C eloqstore_amd sanitize` builds them (also done by
+__graft_entry__.build()); a missing binary is built here.
+"""
+import os
+import subprocess
+
+import pytest
+
+import eloqstore_amd as pcs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPP = os.path.join(ROOT, "tests", "cpp")
+BINS = ("host_logic_test_asan", "host_logic_test_tsan", "capi_sanitize_test")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not all(os.path.exists(os.path.join(CPP, b)) for b in BINS):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "eloqstore_amd"), "sanitize"], check=True,
+                       capture_output=True, timeout=600)
+
+
+def run(name, **env):
+    e = dict(os.environ)
+    e.update(env)
+    r = subprocess.run([os.path.join(CPP, name)], capture_output=True, text=True, timeout=300, env=e)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out
+    assert "ERROR: AddressSanitizer" not in out and "runtime error:" not in out, out
+    assert "WARNING: ThreadSanitizer" not in out, out
+    return out
+
+
+def test_region_registry_asan_ubsan():
+    out = run("host_logic_test_asan", ASAN_OPTIONS="detect_leaks=1:halt_on_error=1",
+              UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    assert "all checks passed" in out
+
+
+def test_region_registry_tsan():
+    out = run("host_logic_test_tsan", TSAN_OPTIONS="halt_on_error=1")
+    assert "all checks passed" in out
+
+
+@pytest.mark.skipif(pcs.device_count() > 0, reason="drives the no-GPU paths")
+def test_capi_host_code_asan_ubsan():
+    out = run("capi_sanitize_test", ASAN_OPTIONS="detect_leaks=1:halt_on_error=1",
+              UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    assert "all checks passed" in out
