@@ -49,7 +49,7 @@ namespace pcs {
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   unsigned long long* first_bad, int ntout) {
+                                                   unsigned long long* first_bad) {
     static_assert(MODE != kStamp, "stamps run as digest + k_scatter_stamp");
     __shared__ uint64_t tile_h[16];
     __shared__ uint8_t tile_ok[16];
@@ -73,8 +73,8 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
         __syncthreads();
         const uint64_t i = t * 16 + threadIdx.x;
         if (threadIdx.x < 16 && i < n) {
-            if (MODE == kDigest || out) st_out(out + i, tile_h[threadIdx.x], ntout);
-            if (MODE == kValidate) st_out(ok + i, tile_ok[threadIdx.x], ntout);
+            if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
+            if (MODE == kValidate) st_nt(ok + i, tile_ok[threadIdx.x]);
         }
         if (MODE == kValidate && first_bad && threadIdx.x == 0) {
             // one note per tile: its smallest failing page
@@ -162,7 +162,7 @@ __device__ __forceinline__ void xxh3_split_tile(const Xxh3Lane& L, PageAt page_a
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   unsigned long long* first_bad, int ntout) {
+                                                   unsigned long long* first_bad) {
     constexpr int PPB = 16 / (P / 4096);  // pages per 256-thread block
     __shared__ uint64_t S[64 * 8];        // block sums per accumulator pair (even, odd)
     __shared__ uint64_t C[16];            // first input word of each slice (the previous block's carry)
@@ -183,8 +183,8 @@ __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ 
         __syncthreads();
         const uint64_t i0 = t * PPB;
         if (threadIdx.x < PPB && i0 + threadIdx.x < n) {
-            if (MODE == kDigest || out) st_out(out + i0 + threadIdx.x, tile_h[threadIdx.x], ntout);
-            if (MODE == kValidate) st_out(ok + i0 + threadIdx.x, tile_ok[threadIdx.x], ntout);
+            if (MODE == kDigest || out) st_nt(out + i0 + threadIdx.x, tile_h[threadIdx.x]);
+            if (MODE == kValidate) st_nt(ok + i0 + threadIdx.x, tile_ok[threadIdx.x]);
         }
         if (MODE == kValidate && first_bad && threadIdx.x == 0) {
             for (int k = 0; k < PPB && i0 + k < n; ++k)
@@ -220,12 +220,14 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
 // fast-path shape are left to k_generic_desc.  Measured alternatives, all
 // bit-exact and all slower on config 3: 4 KiB slices dealt
 // to the groups in rounds (-8 %), byte-budget slice windows (-12..-30 %),
-// per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %).
+// per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %);
+// round 2 (commit 99804f2): pages dealt to a wave's groups as they free up
+// (+-1 %), a wave's pages as a stream of adjacent 4 KiB slices (-5..-8 %).
 template <int MODE, bool NT, bool B4>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad, int ntout) {
+                                                  unsigned long long* first_bad) {
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
@@ -239,337 +241,9 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                 const uint8_t* page = base + o;
                 uint64_t stored = 0;
                 const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
-                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad, ntout);
+                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
             }
         }
-    }
-}
-
-// Descriptor batch (mixed sizes), pages dealt to the groups of a wave as
-// they free up.  Each wave owns LIST consecutive pages; its four groups start
-// on the first four and, whenever a group finishes a page, it takes the next
-// unstarted page of the list (a wave-uniform counter advanced by ballot, no
-// atomics, no LDS on the load path).  Every step a busy group loads one 4 KiB
-// slice of its page (4 blocks + the carry chunk), so the wave keeps its 16 KiB
-// of loads in flight until the list runs dry, instead of idling the groups of
-// shorter pages while the longest page of a 4-page tile finishes (one group
-// per page: ~65 % of group-steps busy on config 3's 4/8/16 KiB mix).  Digests
-// and verdicts are staged per wave in LDS and stored as one coalesced nt
-// store per list.  Pages off the fast shape are left to k_generic_desc.
-template <int MODE, bool NT, int LIST>
-__device__ __forceinline__ void xxh3_desc_wave_body(const uint8_t* __restrict__ base,
-                                                    const uint64_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ len, uint64_t n,
-                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                    unsigned long long* first_bad, int ntout) {
-    static_assert(MODE != kStamp, "descriptor stamps use k_xxh3_desc");
-    static_assert(LIST >= 4 && LIST <= 64, "one list entry per lane");
-    __shared__ uint64_t wave_h[4][LIST];
-    __shared__ uint8_t wave_st[4][LIST];  // 0 bad, 1 good, 2 not on the fast path
-    // wave index made scalar so the list bounds and counter live in SGPRs
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), grp = lane >> 4;
-    const Xxh3Lane L = make_xxh3_lane(lane & 15);
-    // Keys needed once per page (initial accumulators, merge, last stripe) are
-    // re-read from constant memory where used instead of held in VGPRs across
-    // the loop; the opaque index keeps the compiler from hoisting them.
-    auto pair_idx = [&]() {
-        int p2 = 2 * (lane & 3);
-        asm volatile("" : "+v"(p2));
-        return p2;
-    };
-    const uint64_t nblk = (n + 4 * LIST - 1) / (4 * LIST);
-    const uint64_t blk = gridDim.x == nblk ? xcd_tile(blockIdx.x, nblk) : blockIdx.x;
-    const uint64_t b0 = (blk * 4 + wv) * LIST;  // the wave's list: pages [b0, e0)
-    if (b0 >= n) return;                         // wave-uniform; no block barriers below
-    const uint64_t e0 = n - b0 < (uint64_t)LIST ? n : b0 + LIST;
-    uint64_t* hs = wave_h[wv];
-    uint8_t* st = wave_st[wv];
-
-    // per-group state (uniform across the group's 16 lanes)
-    uint64_t Ae = 0, Ao = 0, stored = 0;
-    uint32_t j = (uint32_t)grp;  // list index of this group's page
-    const uint32_t nl = (uint32_t)(e0 - b0);
-    const u32x4* pbase = nullptr;
-    int NB = 0, R = 0, b = 0;
-    uint32_t P = 0;
-    bool fast = false;
-    u32x4 head = {0, 0, 0, 0};
-    auto start = [&]() {
-        if (j >= nl) return;
-        const uint64_t o = off[b0 + j];
-        P = len[b0 + j];
-        fast = xxh3_fast_ok(o, P);
-        if (!fast) return;
-        NB = (int)((P - 9) / 1024);
-        R = (int)(P / 256) - 4 * NB;
-        b = 0;
-        pbase = reinterpret_cast<const u32x4*>(base + o) + L.g;
-        head = ld16<NT>(pbase);
-        stored = lo64(head);
-        const int p2 = pair_idx();
-        Ae = c_init_acc[p2];
-        Ao = c_init_acc[p2 + 1];
-    };
-    start();
-    uint32_t next = 4;  // list index of the first unstarted page (wave-uniform)
-    for (;;) {
-        const bool active = j < nl;
-        if (__ballot(active) == 0) break;
-        if (active && fast) {
-            // one step: blocks b .. b+3 that exist, plus chunk 0 of block b+4 (the carry)
-            u32x4 d[5][4];
-            d[0][0] = head;
-#pragma unroll
-            for (int i = 0; i <= 4; ++i) {
-                const int bb = b + i;
-                const int nc = (bb > NB) ? 0 : (i == 4) ? 1 : (bb == NB) ? R : 4;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (c < nc && !(i == 0 && c == 0)) d[i][c] = ld16<NT>(pbase + bb * 64 + c * 16);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int bb = b + i;
-                uint64_t Te, To;
-                if (bb < NB) {
-                    xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
-                    Ae = xxh3_scramble(Ae + Te, L.ks_e);
-                    Ao = xxh3_scramble(Ao + To, L.ks_o);
-                } else if (bb == NB) {
-                    Xxh3Lane Lf = L;
-                    const int p2 = pair_idx();
-                    Lf.kl0 = c_keys.last[p2];
-                    Lf.kl1 = c_keys.last[p2 + 1];
-                    xxh3_block_terms<true>(Lf, d[i], 0, R, Te, To);
-                    Ae += Te;
-                    Ao += To;
-                }
-            }
-            head = d[4][0];
-            b += 4;
-        }
-        const bool done = active && (!fast || b > NB);
-        if (done) {
-            if (fast) {
-                Xxh3Lane Lm = L;
-                const int p2 = pair_idx();
-                Lm.km_e = c_keys.merge[p2];
-                Lm.km_o = c_keys.merge[p2 + 1];
-                const uint64_t h = xxh3_merge(Lm, Ae, Ao, (uint64_t)(P - 8));
-                if (L.g == 0) {
-                    hs[j] = h;
-                    st[j] = (h == stored) ? 1 : 0;
-                }
-            } else if (L.g == 0) {
-                st[j] = 2;
-            }
-        }
-        // finishing groups take the next pages of the list, in group order
-        const uint64_t fin = __ballot(done);
-        if (done) {
-            j = next + (uint32_t)(__popcll(fin & ((1ull << (16 * grp)) - 1)) >> 4);
-            start();
-        }
-        next += (uint32_t)(__popcll(fin) >> 4);
-    }
-    // LDS writes above came from group leaders of this wave; make them
-    // visible to every lane of the wave before the coalesced store
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t i = b0 + lane;
-    const bool mine = lane < LIST && i < e0;
-    const int s = mine ? st[lane] : 2;
-    if (mine && s != 2) {
-        if (MODE == kDigest || out) st_out(out + i, hs[lane], ntout);
-        if (MODE == kValidate) st_out(ok + i, (uint8_t)s, ntout);
-    }
-    if (MODE == kValidate && first_bad) {
-        const uint64_t bad = __ballot(mine && s == 0);
-        if (bad && lane == 0) note_bad(first_bad, b0 + (uint64_t)(__ffsll((long long)bad) - 1));
-    }
-}
-
-template <int MODE, bool NT, int LIST>
-__global__ __launch_bounds__(256) void k_xxh3_desc_wave(const uint8_t* __restrict__ base,
-                                                       const uint64_t* __restrict__ off,
-                                                       const uint32_t* __restrict__ len, uint64_t n,
-                                                       uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                       unsigned long long* first_bad, int ntout) {
-    xxh3_desc_wave_body<MODE, NT, LIST>(base, off, len, n, out, ok, first_bad, ntout);
-}
-
-// the same with the register budget of 4 waves per SIMD (<= 128 VGPRs)
-template <int MODE, bool NT, int LIST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_xxh3_desc_wave_o4(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off, const uint32_t* __restrict__ len, uint64_t n,
-    uint64_t* __restrict__ out, uint8_t* __restrict__ ok, unsigned long long* first_bad, int ntout) {
-    xxh3_desc_wave_body<MODE, NT, LIST>(base, off, len, n, out, ok, first_bad, ntout);
-}
-
-// Descriptor batch (mixed sizes) as a stream of 4 KiB slices.  A wave owns
-// LIST consecutive pages; their slices (ceil(P / 4096) each, in page order)
-// are dealt round by round to the wave's four groups, so every wave-round
-// loads four ADJACENT slices: 16 KiB of contiguous arena when the pages are
-// packed, the split-page kernel's read pattern, whatever the page sizes.  A
-// group folds its slice's four 1 KiB blocks into block sums (xxhash.h:5988-
-// 6017; the slice's last block leaves its carry word to the next slice) kept
-// in a per-wave LDS ring; the group that folds a page's last slice then runs
-// the page's serial scramble chain over the ring and the merge.  Slice ->
-// page lookup is a ballot over the lanes' exclusive slice prefixes (lane l
-// holds page b0 + l), so the loads carry no extra dependent reads.  Pages of
-// up to 64 KiB on the fast shape; others are left to k_generic_desc
-// (filter 3).
-constexpr int kSliceRing = 32;  // slices resident per wave: a 16-slice page + a round, rounded up
-
-template <int MODE, bool NT, int LIST>
-__global__ __launch_bounds__(256) void k_xxh3_desc_slices(const uint8_t* __restrict__ base,
-                                                         const uint64_t* __restrict__ off,
-                                                         const uint32_t* __restrict__ len, uint64_t n,
-                                                         uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                         unsigned long long* first_bad, int ntout) {
-    static_assert(MODE != kStamp, "descriptor stamps use k_xxh3_desc");
-    static_assert(LIST >= 4 && LIST <= 64, "one page per lane");
-    __shared__ uint64_t ring_s[4][kSliceRing][32];  // [wave][slot][block * 8 + pair * 2 + e/o]
-    __shared__ uint64_t ring_c[4][kSliceRing];      // first word of each slice (the carry of the one before)
-    __shared__ uint64_t wave_h[4][LIST];
-    __shared__ uint8_t wave_st[4][LIST];  // 0 bad, 1 good, 2 not on this path
-    __shared__ uint64_t list_off[4][LIST];  // the wave's pages: offset, length, first slice
-    __shared__ uint32_t list_len[4][LIST];
-    __shared__ uint32_t list_pre[4][LIST];
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), grp = lane >> 4;
-    const int g = lane & 15, p = g & 3;
-    const Xxh3Lane L = make_xxh3_lane(g);
-    const uint64_t nblk = (n + 4 * LIST - 1) / (4 * LIST);
-    const uint64_t blk = gridDim.x == nblk ? xcd_tile(blockIdx.x, nblk) : blockIdx.x;
-    const uint64_t b0 = (blk * 4 + wv) * LIST;  // the wave's pages [b0, b0 + nl)
-    if (b0 >= n) return;                         // wave-uniform; no block barriers below
-    const int nl = (int)(n - b0 < (uint64_t)LIST ? n - b0 : LIST);
-    uint64_t (*S)[32] = ring_s[wv];
-    uint64_t* C = ring_c[wv];
-
-    // lane l: page b0 + l, its slice count and exclusive slice prefix (kept
-    // in LDS, not VGPRs, across the round loop)
-    uint32_t total;
-    {
-        uint64_t o = 0;
-        uint32_t P = 0, c = 0;
-        if (lane < nl) {
-            o = off[b0 + lane];
-            P = len[b0 + lane];
-            if (xxh3_slice_ok(o, P)) c = (P + 4095u) / 4096u;
-            else wave_st[wv][lane] = 2;
-        }
-        uint32_t pre = c;  // inclusive scan over the wave, then exclusive
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t v = __shfl_up(pre, d, 64);
-            if (lane >= d) pre += v;
-        }
-        total = __builtin_amdgcn_readfirstlane(__shfl(pre, 63, 64));
-        if (lane < LIST) {
-            list_off[wv][lane] = o;
-            list_len[wv][lane] = P;
-            list_pre[wv][lane] = pre - c;
-        }
-    }
-    const uint32_t rounds = (total + 3) / 4;
-
-    for (uint32_t r = 0; r < rounds; ++r) {
-        // slice s = 4r + grp: its page = the last list entry whose prefix <= s
-        const uint32_t pre_l = lane < nl ? list_pre[wv][lane] : 0xFFFFFFFFu;
-        uint64_t m[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) m[k] = __ballot(pre_l <= 4 * r + k);
-        const uint32_t s = 4 * r + grp;
-        const bool live = s < total;
-        const uint64_t mk = grp == 0 ? m[0] : grp == 1 ? m[1] : grp == 2 ? m[2] : m[3];
-        const int pl = 63 - __clzll(mk | 1);  // page entry (the |1 keeps a dead group in range)
-        if (live) {
-            const uint64_t po = list_off[wv][pl];
-            const uint32_t P = list_len[wv][pl];
-            const uint32_t ps0 = list_pre[wv][pl];  // the page's first slice
-            const uint32_t pc = (P + 4095u) / 4096u;
-            const int j = (int)(s - ps0);        // slice within the page
-            const int NB = (int)((P - 9) / 1024);  // full blocks; block NB is the final one
-            const int R = (int)(P / 256) - 4 * NB;
-            const u32x4* src = reinterpret_cast<const u32x4*>(base + po + 4096ull * j) + g;
-            u32x4 d[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int b = 4 * j + i;
-                const int nc = b < NB ? 4 : b == NB ? R : 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (c < nc) d[i][c] = ld16<NT>(src + i * 64 + c * 16);
-            }
-            const int slot = (int)(s & (kSliceRing - 1));
-            if (g == 0) C[slot] = lo64(d[0][0]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int b = 4 * j + i;
-                uint64_t Te = 0, To = 0;
-                if (b < NB) {
-                    if (i < 3) {
-                        xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
-                    } else {
-                        xxh3_block_terms<false, true>(L, d[i], 0, 4, Te, To);  // carry from the next slice
-                    }
-                } else if (b == NB) {
-                    Xxh3Lane Lf = L;
-                    const int p2 = opaque_pair_index(g);
-                    Lf.kl0 = c_keys.last[p2];
-                    Lf.kl1 = c_keys.last[p2 + 1];
-                    xxh3_block_terms<true>(Lf, d[i], 0, R, Te, To);
-                }
-                if (g < 4 && b <= NB) {
-                    S[slot][i * 8 + p * 2] = Te;
-                    S[slot][i * 8 + p * 2 + 1] = To;
-                }
-            }
-            if ((uint32_t)j + 1 == pc) {
-                // the page's last slice: serial chain over its blocks, then merge
-                const uint64_t k22 = c_keys.acc[22];
-                const int p2 = opaque_pair_index(g);
-                const uint64_t ks_e = c_keys.scr[p2], ks_o = c_keys.scr[p2 + 1];
-                uint64_t Ae = c_init_acc[p2], Ao = c_init_acc[p2 + 1];
-                for (int b = 0; b < NB; ++b) {
-                    const int sl = (int)((ps0 + (uint32_t)(b >> 2)) & (kSliceRing - 1));
-                    uint64_t Te = S[sl][(b & 3) * 8 + p * 2], To = S[sl][(b & 3) * 8 + p * 2 + 1];
-                    if ((b & 3) == 3 && p == 3) {  // slice boundary: the carry word's two terms
-                        const uint64_t cw = C[(ps0 + (uint32_t)(b >> 2) + 1) & (kSliceRing - 1)];
-                        Te += cw;
-                        To += mul32x32(cw ^ k22);
-                    }
-                    Ae = xxh3_scramble(Ae + Te, ks_e);
-                    Ao = xxh3_scramble(Ao + To, ks_o);
-                }
-                const int sl = (int)((ps0 + (uint32_t)(NB >> 2)) & (kSliceRing - 1));
-                Xxh3Lane Lm = L;
-                Lm.km_e = c_keys.merge[p2];
-                Lm.km_o = c_keys.merge[p2 + 1];
-                const uint64_t h = xxh3_merge(Lm, Ae + S[sl][(NB & 3) * 8 + p * 2],
-                                              Ao + S[sl][(NB & 3) * 8 + p * 2 + 1], (uint64_t)(P - 8));
-                if (g == 0) {
-                    wave_h[wv][pl] = h;
-                    wave_st[wv][pl] = (h == C[ps0 & (kSliceRing - 1)]) ? 1 : 0;
-                }
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t i = b0 + lane;
-    const bool mine = lane < nl;
-    const int st = mine ? wave_st[wv][lane] : 2;
-    if (mine && st != 2) {
-        if (MODE == kDigest || out) st_out(out + i, wave_h[wv][lane], ntout);
-        if (MODE == kValidate) st_out(ok + i, (uint8_t)st, ntout);
-    }
-    if (MODE == kValidate && first_bad) {
-        const uint64_t bad = __ballot(mine && st == 0);
-        if (bad && lane == 0) note_bad(first_bad, b0 + (uint64_t)(__ffsll((long long)bad) - 1));
     }
 }
 
@@ -1096,7 +770,6 @@ __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict_
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (filter == 1 && (algo == 0 ? xxh3_fast_ok(off[i], len[i]) : xxh64_fast_ok(off[i], len[i]))) continue;
         if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
-        if (filter == 3 && xxh3_slice_ok(off[i], len[i])) continue;
         generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
     }
 }
@@ -1622,12 +1295,14 @@ namespace {
 constexpr int kTuneKeys = 20;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
-// sort, 12 descriptor slices, 14 XXH64 descriptor sort, 17 pipelined split
-// tiles (2 or 4 tiles per workgroup, next tile's loads in flight during the
-// chain: -2..-6 % at 2, -13..-22 % at 4, profiles/r02/split_pipe_lab.txt).
+// sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
+// (commit 99804f2): 16 pages dealt to a wave's groups as they free up (+-1 %,
+// profiles/r02/desc_wave_lab.txt), 17 pipelined split tiles (-2..-22 %,
+// split_pipe_lab.txt), 18 plain result stores (+-0.2 %, result_store_lab.txt),
+// 19 descriptor pages as a slice stream (-5..-8 %, desc_slices_lab.txt).
 // Setting one fails.
-constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false,
-                                      false, false, true,  false, true, false, true, false, false, true, false, false};
+constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false,
+                                      true,  false, true,  false, true,  false, true,  true,  true,  true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1638,10 +1313,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*manifest: wide block sums + chain kernel*/ 1,
                                           /*retired*/ 0,
                                           /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4,
-                                          /*xxh3 descriptors: pages per wave list (16/32/64; else one group per page)*/ 0,
-                                          /*retired*/ 0,
-                                          /*results (digests / verdicts) stored non-temporal (1) or plain (0)*/ 1,
-                                          /*xxh3 descriptors: slices dealt per wave, pages per wave list (16/32/64; 0 off)*/ 0};
+                                          /*retired*/ 0, /*retired*/ 0, /*retired*/ 0, /*retired*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1665,7 +1337,6 @@ unsigned page_grid(uint64_t n, unsigned pages_per_block, int key, uint64_t page_
     return (unsigned)(need < cap ? (need ? need : 1) : cap);
 }
 bool use_nt() { return g_tune[3].load(std::memory_order_relaxed) != 0; }
-int nt_out() { return g_tune[18].load(std::memory_order_relaxed) != 0 ? 1 : 0; }
 // Fixed-size XXH3 pages hashed by k_xxh3_split (PCS_TUNE_XXH3_SPLIT_PAGES).
 bool split_pages(uint64_t P) {
     const int64_t split = g_tune[9].load(std::memory_order_relaxed);
@@ -1715,7 +1386,7 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
         const unsigned g = (unsigned)std::min<uint64_t>(need, 0x7FFFFFFFull);
         switch (P) {
 #define CASE(SZ) \
-    case SZ: hipLaunchKernelGGL((k_xxh3_split<SZ, MODE, NT>), dim3(g), dim3(kBlock), 0, s, pages, n, out, ok, fb, nt_out()); break;
+    case SZ: hipLaunchKernelGGL((k_xxh3_split<SZ, MODE, NT>), dim3(g), dim3(kBlock), 0, s, pages, n, out, ok, fb); break;
             CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
         }
@@ -1724,7 +1395,7 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
     switch (P) {
 #define CASE(SZ)                                                                                             \
     case SZ:                                                                                                 \
-        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb, nt_out()); \
+        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb);     \
         break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
@@ -1829,47 +1500,10 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
     if (n == 0) return hipSuccess;
     if (skip == 8 && seed == 0) {
         // fast kernels for conforming pages, generic lanes for the rest
-        const int64_t wl = g_tune[16].load(std::memory_order_relaxed);
-        const int64_t wlist = wl & ~int64_t(1);  // odd value: the 4-waves-per-SIMD register budget
-        const int64_t sl = g_tune[19].load(std::memory_order_relaxed);
-        int gfilter = 1;  // generic lanes take the pages the fast kernel leaves
-        if (algo == 0 && MODE != kStamp && (sl == 16 || sl == 32 || sl == 64)) {
-            // slices dealt round by round to a wave's groups (PCS_TUNE_XXH3_DESC_SLICES)
-            const uint64_t nblk = (n + 4 * (uint64_t)sl - 1) / (4 * (uint64_t)sl);
-            if (nblk > 0x7FFFFFFFull) return hipErrorNotSupported;
-            const bool nt = use_nt();
-            constexpr int KM = MODE == kStamp ? kDigest : MODE;
-#define LS(NT_, LIST_)                                                                                              \
-    hipLaunchKernelGGL((k_xxh3_desc_slices<KM, NT_, LIST_>), dim3((unsigned)nblk), dim3(kBlock), 0, s, base, off, len, \
-                       n, out, ok, fb, nt_out())
-            if (sl == 16) { if (nt) LS(true, 16); else LS(false, 16); }
-            else if (sl == 32) { if (nt) LS(true, 32); else LS(false, 32); }
-            else { if (nt) LS(true, 64); else LS(false, 64); }
-#undef LS
-            gfilter = 3;
-        } else if (algo == 0 && MODE != kStamp && (wlist == 16 || wlist == 32 || wlist == 64)) {
-            // pages dealt to the groups of a wave as they free up (PCS_TUNE_XXH3_DESC_WAVE_LIST)
-            const uint64_t nblk = (n + 4 * (uint64_t)wlist - 1) / (4 * (uint64_t)wlist);
-            if (nblk > 0x7FFFFFFFull) return hipErrorNotSupported;
-            const bool nt = use_nt(), o4 = (wl & 1) != 0;
-            constexpr int KM = MODE == kStamp ? kDigest : MODE;
-#define LW(NT_, LIST_)                                                                                             \
-    do {                                                                                                           \
-        if (o4)                                                                                                    \
-            hipLaunchKernelGGL((k_xxh3_desc_wave_o4<KM, NT_, LIST_>), dim3((unsigned)nblk), dim3(kBlock), 0, s, base, \
-                               off, len, n, out, ok, fb, nt_out());                                                \
-        else                                                                                                       \
-            hipLaunchKernelGGL((k_xxh3_desc_wave<KM, NT_, LIST_>), dim3((unsigned)nblk), dim3(kBlock), 0, s, base,  \
-                               off, len, n, out, ok, fb, nt_out());                                                \
-    } while (0)
-            if (wlist == 16) { if (nt) LW(true, 16); else LW(false, 16); }
-            else if (wlist == 32) { if (nt) LW(true, 32); else LW(false, 32); }
-            else { if (nt) LW(true, 64); else LW(false, 64); }
-#undef LW
-        } else if (algo == 0) {
+        if (algo == 0) {
             const unsigned grid = page_grid(n, kBlock / 16, 1);
 #define L(NT_, B4_) \
-    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb, nt_out())
+    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
             if (use_nt()) {
                 if (rt_batch4()) L(true, true);
                 else L(true, false);
@@ -1893,7 +1527,7 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
         if (e != hipSuccess) return e;
         const unsigned grid = grid_for(n, kBlock, kBlocksPerCu);
         hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip,
-                           gfilter, out, ok, fb);
+                           1, out, ok, fb);
         return hipGetLastError();
     }
     int filter = 0;

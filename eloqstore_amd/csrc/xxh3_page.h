@@ -53,14 +53,7 @@ __device__ __forceinline__ uint64_t hi64(u32x4 v) { return ((uint64_t)v.w << 32)
 // (profiles/r01/read_lab_stores.txt).
 template <typename T>
 __device__ __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
-// Staged per-tile result store: nt, or plain so that the partial lines of
-// neighbouring tiles (same XCD, adjacent results) merge in L2 before they are
-// written back (PCS_TUNE_RESULT_NT).
-template <typename T>
-__device__ __forceinline__ void st_out(T* p, T v, int nt) {
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+
 
 // first_bad = min(first_bad, idx).  The word only ever decreases, so a stale
 // (larger) read can only cause an unneeded atomic, never skip a needed one;
@@ -72,17 +65,17 @@ __device__ __forceinline__ void note_bad(unsigned long long* first_bad, uint64_t
 }
 
 __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_t stored, uint8_t* page_w,
-                                     uint64_t* out, uint8_t* ok, unsigned long long* first_bad, int ntout = 1) {
+                                     uint64_t* out, uint8_t* ok, unsigned long long* first_bad) {
     if (mode == kStamp) {
         st_nt(reinterpret_cast<uint64_t*>(page_w), h);
-        if (out) st_out(out + idx, h, ntout);
+        if (out) st_nt(out + idx, h);
     } else if (mode == kValidate) {
         const bool good = (h == stored);
-        st_out(ok + idx, (uint8_t)(good ? 1 : 0), ntout);
-        if (out) st_out(out + idx, h, ntout);
+        st_nt(ok + idx, (uint8_t)(good ? 1 : 0));
+        if (out) st_nt(out + idx, h);
         if (!good && first_bad) note_bad(first_bad, idx);
     } else {
-        st_out(out + idx, h, ntout);
+        st_nt(out + idx, h);
     }
 }
 
@@ -134,15 +127,6 @@ __device__ __forceinline__ Xxh3Lane make_xxh3_lane(int g) {
     L.init_e = c_init_acc[2 * gl];
     L.init_o = c_init_acc[2 * gl + 1];
     return L;
-}
-
-// 2 * (g & 3) behind an empty asm, so a key table read indexed by it is done
-// where it is written (once per page) instead of being hoisted and held in
-// VGPRs across a kernel's main loop.
-__device__ __forceinline__ int opaque_pair_index(int g) {
-    int p2 = 2 * (g & 3);
-    asm volatile("" : "+v"(p2));
-    return p2;
 }
 
 // Fold one 1 KiB block (chunks 0..nchunks-1 present) into the sums (Te, To)
@@ -327,8 +311,6 @@ __device__ __forceinline__ uint64_t xxh3_page_rt4(const uint8_t* __restrict__ pa
 __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
     return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
 }
-// pages the slice-stream descriptor kernel takes (k_xxh3_desc_slices)
-__device__ __forceinline__ bool xxh3_slice_ok(uint64_t off, uint32_t P) { return xxh3_fast_ok(off, P) && P <= 65536u; }
 
 // Tile t of nb -> renumbered so that the blocks of one XCD (blockIdx % 8)
 // walk one contiguous eighth of the batch (cdna_hip_programming.md T1,

@@ -234,24 +234,11 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
  *                                     kernel (1, 2 or 4; 16 pages per wave)
- *   PCS_TUNE_XXH3_DESC_WAVE_LIST  [0] XXH3 descriptor batches: 16, 32 or 64
- *                                     pages per wave list, dealt to the
- *                                     wave's four groups as they free up
- *                                     (k_xxh3_desc_wave); 0 = one group per
- *                                     page, 16-page tiles (k_xxh3_desc)
- *   PCS_TUNE_RESULT_NT            [1] XXH3 page kernels store digests and
- *                                     verdicts non-temporal (1) or with plain
- *                                     stores that merge in L2 (0)
- *   PCS_TUNE_XXH3_DESC_SLICES     [0] XXH3 descriptor batches as a stream of
- *                                     4 KiB slices: 16, 32 or 64 pages per
- *                                     wave, slices dealt round by round to the
- *                                     wave's groups (k_xxh3_desc_slices;
- *                                     pages up to 64 KiB); 0 = off
- * Keys 4, 5, 10, 12, 14 and 17 selected variants that measured slower (XXH64 quad
- * nt loads, in-place stamp widths, descriptor tile sorts and 4 KiB slices,
- * pipelined split-page tiles);
- * they were retired in round 2: setting one fails and reading
- * one returns -1. */
+ * Keys 4, 5, 10, 12, 14 and 16-19 selected variants that measured slower or no
+ * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
+ * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
+ * tiles, plain result stores); they were retired in round 2:
+ * setting one fails and reading one returns -1. */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -263,9 +250,6 @@ enum pcs_tune_key {
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_WAVES = 15,
-    PCS_TUNE_XXH3_DESC_WAVE_LIST = 16,
-    PCS_TUNE_RESULT_NT = 18,
-    PCS_TUNE_XXH3_DESC_SLICES = 19,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
