@@ -22,7 +22,11 @@ Also reported, on the same line:
                 time (HIP events on the launch stream) vs 8 TB/s HBM peak;
                 traffic = PMC-measured HBM bytes per launch from the committed
                 rocprofv3 summary under profiles/ (else null).
-  read_ceiling  a plain streaming read of the same buffer (no hash).
+  stream_read   the fastest plain streaming read of the same buffer we could
+                write (pcs_stream_read_dev, no hash): the practical read rate
+                of the part, within ~1 % of the hash kernels on 4 KiB pages
+                (profiles/r02/stream_sleep_lab.txt); context, not the roofline
+                peak (that is the 8 TB/s spec).
   cpu_baseline  BASELINE config 1: the reference's own xxHash (oracle/_ref) on
                 ONE host thread, reading every page of a 1 GiB file of 4 KiB
                 pages and validating it like page_checksum_tool / page.cpp:25-31;
@@ -197,9 +201,9 @@ class Workload:
         # 8 B digest (digest), 1 B verdict (validate), 8 B into the page (stamp)
         return self.bytes + (1 if mode == "validate" else 8) * self.n
 
-    def read_ceiling(self, reps: int) -> float | None:
-        """The same bytes read by the plain streaming-read kernel (no hash):
-        pcs_stream_read_dev over the whole batch buffer."""
+    def stream_read(self, reps: int) -> float | None:
+        """GB/s of the batch buffer read by the plain streaming-read kernel
+        (no hash): pcs_stream_read_dev over the whole buffer."""
         scratch = torch.empty((self.bytes + 65535) // 65536, dtype=torch.int64, device=self.dev)
 
         def run():
@@ -214,7 +218,7 @@ class Workload:
         ev[1].record()
         torch.cuda.synchronize()
         t = ev[0].elapsed_time(ev[1]) / 1e3 / reps
-        return self.algorithmic_bytes() / t / 1e9
+        return self.bytes / t / 1e9
 
     def sample_pages_host(self, max_bytes: int):
         """(host uint8 array, page size, gpu digests) for a leading sample of the batch."""
@@ -658,7 +662,7 @@ def main():
         w.step("digest")
         torch.cuda.synchronize()
     parity = parity_sample(w) if rank == 0 else None
-    ceiling = w.read_ceiling(max(3, args.steps // 20))
+    stream_rate = w.stream_read(max(3, args.steps // 20))
     time.sleep(PHASE_GAP_S)
     drill = w.corruption_drill() if rank == 0 else None
     time.sleep(PHASE_GAP_S)
@@ -712,7 +716,7 @@ def main():
                 "avg_launch_ms": round(avg_launch * 1e3, 4),
                 "launch_timing": f"HIP events bracketing the {args.steps} timed steps on the launch stream",
             },
-            "read_ceiling_GBps": round(ceiling, 1) if ceiling else None,
+            "stream_read_GBps": round(stream_rate, 1) if stream_rate else None,
             "cpu_baseline": c1["cpu_baseline"] if c1 else None,
             "parity": parity,
         }

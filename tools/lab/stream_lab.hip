@@ -76,6 +76,29 @@ __global__ __launch_bounds__(T) void k_win(const uint8_t* __restrict__ buf, uint
     if ((x ^ y) == 0x9E3779B9u) out[w] = x;  // practically never: keeps the loads live
 }
 
+// Layout 1 (the product's groups) with SLEEP x 64 cycles of s_sleep after the
+// window's loads are consumed: the hash kernel spends ~1-2 us of VALU per
+// block after its loads land; does a pure read that idles as long per block
+// stream faster than one that exits at once?
+template <int SLEEP>
+__global__ __launch_bounds__(256) void k_win_sleep(const uint8_t* __restrict__ buf, uint64_t nwin, uint64_t* out) {
+    constexpr int CH = 65536, T = 256, L = CH / (T * 16);
+    const uint64_t w = xcd_tile(blockIdx.x, nwin);
+    const u32x4* base = reinterpret_cast<const u32x4*>(buf + w * (uint64_t)CH);
+    u32x4 d[L];
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+#pragma unroll
+    for (int i = 0; i < L; ++i) d[i] = ld<true>(base + (grp + (i / 16) * (T / 16)) * 256 + (i % 16) * 16 + g);
+    uint32_t x = 0, y = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        x ^= d[i].x ^ d[i].z;
+        y += d[i].y + d[i].w;
+    }
+    for (int k = 0; k < SLEEP; ++k) __builtin_amdgcn_s_sleep(1);
+    if ((x ^ y) == 0x9E3779B9u) out[w] = x;
+}
+
 // The same with dynamic LDS reserved only to cap workgroups per CU (160 KiB
 // of LDS per CU / the reservation), i.e. bytes in flight per CU.
 template <int CH, int T, int LAYOUT>
@@ -172,8 +195,22 @@ int main(int argc, char** argv) {
                       }, {}});
     };
     const bool only_product = argc > 2 && std::string(argv[2]) == "product";
+    const bool sleep_mode = argc > 2 && std::string(argv[2]) == "sleep";
+    for (uint64_t bytes : {uint64_t(4) << 30, big}) {
+        if (!sleep_mode) break;
+        char t[128];
+        auto nm = [&](const char* v) {
+            std::snprintf(t, sizeof t, "%-34s %6.2f GiB", v, bytes / double(1ull << 30));
+            return t;
+        };
+        add_win(nm("win64K groups sleep 0"), bytes, k_win_sleep<0>, 65536, 256);
+        add_win(nm("win64K groups sleep 4x64cyc"), bytes, k_win_sleep<4>, 65536, 256);
+        add_win(nm("win64K groups sleep 16x64cyc"), bytes, k_win_sleep<16>, 65536, 256);
+        add_win(nm("win64K groups sleep 32x64cyc"), bytes, k_win_sleep<32>, 65536, 256);
+        add_win(nm("win64K groups sleep 64x64cyc"), bytes, k_win_sleep<64>, 65536, 256);
+    }
     for (uint64_t bytes : {uint64_t(4) << 30, bytes3 & ~((uint64_t(128) << 10) - 1), big}) {
-        if (only_product) break;
+        if (only_product || sleep_mode) break;
         char t[128];
         auto nm = [&](const char* v) {
             std::snprintf(t, sizeof t, "%-34s %6.2f GiB", v, bytes / double(1ull << 30));
