@@ -488,10 +488,22 @@ SWEEP = (
 PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits the kernel trace on it
 
 
-def sweep(dev: str, steps: int, warmup: int):
+def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None):
+    """Each entry on a device-resident workload that stays allocated until the
+    sweep ends: config 2 entries reuse the headline's batch (`head`), config 3
+    XXH64 reuses config 3's arena.  Nothing is freed between entries: a
+    hipFree of a large buffer (torch.cuda.empty_cache) left every other buffer
+    of the process reading ~1.5 % slower until another process initialised
+    the GPU (tools/lab/degrade_lab.py, profiles/r02/degrade_lab.txt)."""
     out = []
+    resident: dict[int, Workload] = {}
+    if head is not None and head.cfg == 2 and head.n == CONFIGS[2][1]:
+        resident[2] = head
     for key, cfg, algo, mode in SWEEP:
-        w = Workload(cfg, algo, 0, None, dev)
+        if cfg not in resident:
+            resident[cfg] = Workload(cfg, algo, 0, None, dev)
+        w = resident[cfg]
+        w.algo = algo
         if mode == "validate":
             w.step("stamp")
         torch.cuda.synchronize()
@@ -515,9 +527,6 @@ def sweep(dev: str, steps: int, warmup: int):
              "traffic": traffic[0] if traffic else None, "traffic_source": traffic[1] if traffic else None,
              "parity": par, "corruption_drill": drill}
         out.append(e)
-        w.free()
-        del w
-        torch.cuda.empty_cache()
         time.sleep(PHASE_GAP_S)
     return out
 
@@ -669,7 +678,7 @@ def main():
     hostinc = host_inclusive(w) if args.host_inclusive and rank == 0 else None
     sweep_entries = None
     if rank == 0 and world == 1 and not args.no_sweep:
-        sweep_entries = sweep(dev, args.sweep_steps, args.sweep_warmup)
+        sweep_entries = sweep(dev, args.sweep_steps, args.sweep_warmup, head=w if algo == 0 else None)
     c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         c1 = config1(args.cpu_seconds, None if args.no_all_cores else min(args.cpu_seconds, 5.0))
