@@ -54,7 +54,6 @@ __device__ __forceinline__ uint64_t hi64(u32x4 v) { return ((uint64_t)v.w << 32)
 template <typename T>
 __device__ __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
 
-
 // first_bad = min(first_bad, idx).  The word only ever decreases, so a stale
 // (larger) read can only cause an unneeded atomic, never skip a needed one;
 // reading first keeps a batch of mostly corrupt pages from serialising on
@@ -304,69 +303,6 @@ __device__ __forceinline__ uint64_t xxh3_page_rt4(const uint8_t* __restrict__ pa
             }
         }
         head = d[4][0];
-    }
-    return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
-}
-
-// Run-time page size, 4 KiB-ALIGNED steps: step s loads exactly blocks
-// 4s .. 4s+3 (the page's s-th 4 KiB, nothing of the next), so no step's loads
-// straddle a 4 KiB boundary of the page.  The carry word of block 4s+3 (the
-// first word of block 4s+4) therefore arrives with the next step: block 4s+3
-// is folded without it (NOCARRY, like the split kernel's slice ends), its
-// scramble is held back, and the next step adds the carry word's two terms
-// (pair 3; key = secret word 22) before scrambling it.  Same bits as
-// xxh3_page_rt4.
-template <bool NT>
-__device__ __forceinline__ uint64_t xxh3_page_rt4a(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
-                                                   uint64_t& stored) {
-    const int NB = (int)((P - 9) / 1024);
-    const int R = (int)(P / 256) - 4 * NB;
-    const int TB = NB + 1;
-    const int p = L.g & 3;
-    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
-    uint64_t Ae = L.init_e, Ao = L.init_o;
-    uint64_t He = 0, Ho = 0;  // block sums of the previous step's last block, waiting for its carry
-    bool held = false;
-    for (int b0 = 0; b0 < TB; b0 += 4) {
-        u32x4 d[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int b = b0 + i;
-            const int nc = (b > NB) ? 0 : (b == NB) ? R : 4;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c < nc) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
-        }
-        if (b0 == 0) stored = lo64(d[0][0]);
-        if (held) {
-            // carry word = lane 0's low word of chunk 0 of block b0
-            const uint64_t cw = __shfl(lo64(d[0][0]), threadIdx.x & ~15u, 64);
-            if (p == 3) {
-                He += cw;
-                Ho += mul32x32(cw ^ c_keys.acc[22]);
-            }
-            Ae = xxh3_scramble(Ae + He, L.ks_e);
-            Ao = xxh3_scramble(Ao + Ho, L.ks_o);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int b = b0 + i;
-            uint64_t Te, To;
-            if (b < NB) {
-                if (i < 3) {
-                    xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
-                    Ae = xxh3_scramble(Ae + Te, L.ks_e);
-                    Ao = xxh3_scramble(Ao + To, L.ks_o);
-                } else {
-                    xxh3_block_terms<false, true>(L, d[i], 0, 4, He, Ho);
-                }
-            } else if (b == NB) {
-                xxh3_block_terms<true>(L, d[i], 0, R, Te, To);
-                Ae += Te;
-                Ao += To;
-            }
-        }
-        held = (b0 + 3 < NB);
     }
     return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
 }

@@ -234,14 +234,10 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
  *                                     kernel (1, 2 or 4; 16 pages per wave)
- *   PCS_TUNE_XXH3_ALIGNED_STEPS   [0] run-time-size XXH3 pages (descriptor
- *                                     batches): each 4 KiB step loads exactly
- *                                     the page's next 4 KiB, the carry word is
- *                                     taken from the next step (1)
- * Keys 4, 5, 10, 12, 14 and 16-19 selected variants that measured slower or no
+ * Keys 4, 5, 10, 12, 14 and 16-20 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
- * tiles, plain result stores); they were retired in round 2:
+ * tiles, plain result stores, 4 KiB-aligned descriptor steps); they were retired in round 2:
  * setting one fails and reading one returns -1. */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
@@ -254,7 +250,6 @@ enum pcs_tune_key {
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_WAVES = 15,
-    PCS_TUNE_XXH3_ALIGNED_STEPS = 20,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
