@@ -488,7 +488,7 @@ SWEEP = (
 PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits the kernel trace on it
 
 
-def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None):
+def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale: int = 1):
     """Each entry on a device-resident workload that stays allocated until the
     sweep ends: config 2 entries reuse the headline's batch (`head`), config 3
     XXH64 reuses config 3's arena.  Nothing is freed between entries: a
@@ -497,11 +497,11 @@ def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None):
     the GPU (tools/lab/degrade_lab.py, profiles/r02/degrade_lab.txt)."""
     out = []
     resident: dict[int, Workload] = {}
-    if head is not None and head.cfg == 2 and head.n == CONFIGS[2][1]:
+    if head is not None and head.cfg == 2 and head.n == CONFIGS[2][1] // scale:
         resident[2] = head
     for key, cfg, algo, mode in SWEEP:
         if cfg not in resident:
-            resident[cfg] = Workload(cfg, algo, 0, None, dev)
+            resident[cfg] = Workload(cfg, algo, 0, max(1, CONFIGS[cfg][1] // scale), dev)
         w = resident[cfg]
         w.algo = algo
         if mode == "validate":
@@ -580,6 +580,8 @@ def main():
     ap.add_argument("--no-sweep", action="store_true", help="headline only (no per-config sweep)")
     ap.add_argument("--sweep-steps", type=int, default=50)
     ap.add_argument("--sweep-warmup", type=int, default=5)
+    ap.add_argument("--sweep-scale", type=int, default=1,
+                    help="divide every sweep workload's page count (tests only; default 1 = the BASELINE sizes)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the host-memory path (pinned direct DMA and pageable gather)")
     args = ap.parse_args()
@@ -678,7 +680,8 @@ def main():
     hostinc = host_inclusive(w) if args.host_inclusive and rank == 0 else None
     sweep_entries = None
     if rank == 0 and world == 1 and not args.no_sweep:
-        sweep_entries = sweep(dev, args.sweep_steps, args.sweep_warmup, head=w if algo == 0 else None)
+        sweep_entries = sweep(dev, args.sweep_steps, args.sweep_warmup, head=w if algo == 0 else None,
+                              scale=max(1, args.sweep_scale))
     c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         c1 = config1(args.cpu_seconds, None if args.no_all_cores else min(args.cpu_seconds, 5.0))
