@@ -368,9 +368,26 @@ def config1(target_s: float, all_cores_s: float | None, workdir: str | None = No
                     "sample": f"config 1 file, {T} threads (one per usable core: affinity mask capped by the cgroup "
                               f"CPU quota) on disjoint page ranges, "
                               f"~{all_cores_s:.0f} s"}
+        # the same pages through this repo's CPU restatement
+        # (oracle/xxh_oracle.c), in memory, one thread: the port's own rate
+        # and a parity check of it against the stamped headers
+        data = np.fromfile(path, dtype=np.uint8)
+        want = data.reshape(n, P)[:, :8].copy().view(np.uint64).ravel()
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            got = oracle.pages_digest(data, P, 0)
+            reps += 1
+            if time.perf_counter() - t0 >= min(3.0, target_s):
+                break
+        dt = time.perf_counter() - t0
+        port = {"value": round(reps * n * P / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"config 1 file in memory, {reps} passes of oracle/xxh_oracle.c (the repo's C restatement, "
+                          f"gcc -O2) per page, one thread",
+                "pages_failed": int((got != want).sum())}
+        del data
         r = subprocess.run([pcs.TOOL_PATH, "--scan", path, str(P)], capture_output=True, text=True, timeout=300)
         scan = {"rc": r.returncode, "line": r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr.strip()}
-        return {"cpu_baseline": one, "cpu_all_cores": allc, "cli_scan": scan}
+        return {"cpu_baseline": one, "cpu_all_cores": allc, "cpu_port": port, "cli_scan": scan}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -735,6 +752,7 @@ def main():
         line["corruption_drill"] = drill
         if c1 is not None:
             line["cpu_all_cores"] = c1["cpu_all_cores"]
+            line["cpu_port"] = c1["cpu_port"]
             line["cli_scan"] = c1["cli_scan"]
         if scaling is not None:
             line["scaling_detail"] = scaling
