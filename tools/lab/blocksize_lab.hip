@@ -50,6 +50,29 @@ __global__ __launch_bounds__(BT) void k_fixed_bt(const uint8_t* __restrict__ pag
     if (threadIdx.x < TP && t * TP + threadIdx.x < n) st_nt(out + t * TP + threadIdx.x, tile_h[threadIdx.x]);
 }
 
+// the product's descriptor body (one group per page, 4-block steps) with
+// BT / 16 pages per workgroup
+template <int BT>
+__global__ __launch_bounds__(BT) void k_desc_bt(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                               const uint32_t* __restrict__ len, uint64_t n, uint64_t* __restrict__ out) {
+    constexpr int TP = BT / 16;
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const uint64_t ntiles = (n + TP - 1) / TP;
+    const uint64_t t = xcd_tile(blockIdx.x, ntiles);
+    const uint64_t pg = t * TP + (threadIdx.x >> 4);
+    if (pg < n) {
+        uint64_t stored = 0;
+        const uint64_t h = xxh3_page_rt4<true>(base + off[pg], len[pg], L, stored);
+        if (L.g == 0) st_nt(out + pg, h);
+    }
+}
+
+static uint64_t mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 __global__ void k_fill(uint64_t* p, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t z = i + 0x9E3779B97F4A7C15ull;
@@ -88,6 +111,34 @@ int main(int argc, char** argv) {
         add(512, k_fixed_bt<512>);
         add(1024, k_fixed_bt<1024>);
     }
+    // config 3 (1 M mixed 4/8/16 KiB pages packed at the start of the buffer)
+    const uint64_t n3 = 1 << 20;
+    std::vector<uint64_t> off3(n3);
+    std::vector<uint32_t> len3(n3);
+    uint64_t o3 = 0;
+    for (uint64_t p = 0; p < n3; ++p) {
+        const uint64_t cls = mix((0x5EED0003ull ^ p) + (0x5A5A5A5Aull + 1) * 0x9E3779B97F4A7C15ull) % 3;
+        len3[p] = 4096u << cls;
+        off3[p] = o3;
+        o3 += len3[p];
+    }
+    uint64_t* d_off;
+    uint32_t* d_len;
+    CK(hipMalloc(&d_off, n3 * 8));
+    CK(hipMalloc(&d_len, n3 * 4));
+    CK(hipMemcpy(d_off, off3.data(), n3 * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_len, len3.data(), n3 * 4, hipMemcpyHostToDevice));
+    const double bytes3 = (double)o3 + 8.0 * n3;
+    auto add3 = [&](int bt, auto kern) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "config 3 desc %4d threads (%2d pages/WG)", bt, bt / 16);
+        const unsigned g = (unsigned)((n3 + bt / 16 - 1) / (bt / 16));
+        vs.push_back({nm, 0, [=] { hipLaunchKernelGGL(kern, dim3(g), dim3(bt), 0, 0, pages, d_off, d_len, n3, out); }, {}});
+    };
+    add3(64, k_desc_bt<64>);
+    add3(128, k_desc_bt<128>);
+    add3(256, k_desc_bt<256>);
+    add3(512, k_desc_bt<512>);
     // parity: every variant's digests equal the 256-thread ones
     for (uint64_t n : {uint64_t(1) << 20, nbig}) {
         hipLaunchKernelGGL(k_fixed_bt<256>, dim3((unsigned)(n / 16)), dim3(256), 0, 0, pages, n, ref);
@@ -124,7 +175,7 @@ int main(int argc, char** argv) {
     std::printf("%-36s %10s %8s %7s\n", "variant", "med_us", "TB/s", "frac");
     for (auto& v : vs) {
         std::sort(v.us.begin(), v.us.end());
-        const double m = v.us[v.us.size() / 2], bytes = v.n * 4104.0;
+        const double m = v.us[v.us.size() / 2], bytes = v.n ? v.n * 4104.0 : bytes3;
         std::printf("%-36s %10.1f %8.3f %7.4f\n", v.name.c_str(), m, bytes / m / 1e6, bytes / m / 1e6 / 8.0);
     }
     return 0;
