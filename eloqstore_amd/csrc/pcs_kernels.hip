@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
 // per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %);
 // round 2 (commit 99804f2): pages dealt to a wave's groups as they free up
 // (+-1 %), a wave's pages as a stream of adjacent 4 KiB slices (-5..-8 %).
-template <int MODE, bool NT, int B4>
+template <int MODE, bool NT, bool B4>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
@@ -240,9 +240,7 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
             if (xxh3_fast_ok(o, P)) {
                 const uint8_t* page = base + o;
                 uint64_t stored = 0;
-                const uint64_t h = B4 == 2   ? xxh3_page_rt4_lean<NT>(page, P, L, stored)
-                                   : B4 == 1 ? xxh3_page_rt4<NT>(page, P, L, stored)
-                                             : xxh3_page_rt<NT>(page, P, L, stored);
+                const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
                 if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
             }
         }
@@ -1302,11 +1300,11 @@ constexpr int kTuneKeys = 22;
 // profiles/r02/desc_wave_lab.txt), 17 pipelined split tiles (-2..-22 %,
 // split_pipe_lab.txt), 18 plain result stores (+-0.2 %, result_store_lab.txt),
 // 19 descriptor pages as a slice stream (-5..-8 %, desc_slices_lab.txt),
-// 20 4 KiB-aligned descriptor steps (+-0.2 %, aligned_steps_lab.txt, commit
-// after 99804f2).
+// 20 4 KiB-aligned descriptor steps (+-0.2 %, aligned_steps_lab.txt), 21 the
+// descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt).
 // Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false,
-                                      true,  false, true,  false, true,  false, true,  true,  true,  true,  true,  false};
+                                      true,  false, true,  false, true,  false, true,  true,  true,  true,  true,  true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1319,7 +1317,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4,
                                           /*retired*/ 0, /*retired*/ 0, /*retired*/ 0, /*retired*/ 0,
                                           /*retired*/ 0,
-                                          /*xxh3 descriptors: per-page keys from constant memory (128 VGPRs)*/ 0};
+                                          /*retired*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1349,7 +1347,6 @@ bool split_pages(uint64_t P) {
     return split > 0 && P >= (uint64_t)split && P >= 8192 && P <= 65536 && (P & (P - 1)) == 0;
 }
 bool rt_batch4() { return g_tune[8].load(std::memory_order_relaxed) != 0; }
-bool desc_lean() { return g_tune[21].load(std::memory_order_relaxed) != 0; }
 
 // XXH64 LDS kernel launch with the segment depth from PCS_TUNE_XXH64_LAYOUT
 // (0 or 1 = default depth, 2/3/4 = depth 1/2/4) and the waves per workgroup
@@ -1511,15 +1508,12 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             const unsigned grid = page_grid(n, kBlock / 16, 1);
 #define L(NT_, B4_) \
     hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
-            const int rt = rt_batch4() ? (desc_lean() ? 2 : 1) : 0;
             if (use_nt()) {
-                if (rt == 2) L(true, 2);
-                else if (rt == 1) L(true, 1);
-                else L(true, 0);
+                if (rt_batch4()) L(true, true);
+                else L(true, false);
             } else {
-                if (rt == 2) L(false, 2);
-                else if (rt == 1) L(false, 1);
-                else L(false, 0);
+                if (rt_batch4()) L(false, true);
+                else L(false, false);
             }
 #undef L
         } else {

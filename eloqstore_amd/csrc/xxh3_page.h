@@ -307,72 +307,6 @@ __device__ __forceinline__ uint64_t xxh3_page_rt4(const uint8_t* __restrict__ pa
     return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
 }
 
-// 2 * (g & 3) behind an empty asm: a key table read indexed by it is done
-// where it is written (once per page) instead of being hoisted out of the
-// kernel's loops and held in VGPRs.
-__device__ __forceinline__ int opaque_pair_index(int g) {
-    int p2 = 2 * (g & 3);
-    asm volatile("" : "+v"(p2));
-    return p2;
-}
-
-// xxh3_page_rt4 with the per-page keys (initial accumulators, last-stripe and
-// merge keys) read from constant memory where they are used, so the
-// descriptor kernel fits 128 VGPRs (4 waves per SIMD instead of 3).
-template <bool NT>
-__device__ __forceinline__ uint64_t xxh3_page_rt4_lean(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
-                                                       uint64_t& stored) {
-    const int NB = (int)((P - 9) / 1024);
-    const int R = (int)(P / 256) - 4 * NB;
-    const int TB = NB + 1;
-    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
-    uint64_t Ae, Ao;
-    {
-        const int p2 = opaque_pair_index(L.g);
-        Ae = c_init_acc[p2];
-        Ao = c_init_acc[p2 + 1];
-    }
-    u32x4 head = ld16<NT>(base);
-    stored = lo64(head);
-    for (int b0 = 0; b0 < TB; b0 += 4) {
-        u32x4 d[5][4];
-        d[0][0] = head;
-#pragma unroll
-        for (int i = 0; i <= 4; ++i) {
-            const int b = b0 + i;
-            const int nc = (b >= TB) ? 0 : (i == 4) ? 1 : (b == NB) ? R : 4;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c < nc && !(i == 0 && c == 0)) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int b = b0 + i;
-            if (b < NB) {
-                uint64_t Te, To;
-                xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
-                Ae = xxh3_scramble(Ae + Te, L.ks_e);
-                Ao = xxh3_scramble(Ao + To, L.ks_o);
-            } else if (b == NB) {
-                Xxh3Lane Lf = L;
-                const int p2 = opaque_pair_index(L.g);
-                Lf.kl0 = c_keys.last[p2];
-                Lf.kl1 = c_keys.last[p2 + 1];
-                uint64_t Te, To;
-                xxh3_block_terms<true>(Lf, d[i], 0, R, Te, To);
-                Ae += Te;
-                Ao += To;
-            }
-        }
-        head = d[4][0];
-    }
-    Xxh3Lane Lm = L;
-    const int p2 = opaque_pair_index(L.g);
-    Lm.km_e = c_keys.merge[p2];
-    Lm.km_o = c_keys.merge[p2 + 1];
-    return xxh3_merge(Lm, Ae, Ao, (uint64_t)(P - 8));
-}
-
 __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
     return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
 }

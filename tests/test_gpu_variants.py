@@ -29,14 +29,12 @@ VARIANTS = {
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "x64_one_wave": {pcs.TUNE_XXH64_WAVES: 1},
     "x64_two_waves_depth4": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 4},
-    "desc_lean": {pcs.TUNE_XXH3_DESC_LEAN: 1},
-    "desc_lean_no_nt": {pcs.TUNE_XXH3_DESC_LEAN: 1, pcs.TUNE_NT_LOADS: 0},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = [k for k in range(1, 22) if pcs.get_tuning(k) >= 0]  # retired keys read -1
+    keys = [k for k in range(1, 16) if pcs.get_tuning(k) >= 0]  # retired keys read -1
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -68,7 +66,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_one_wave",
-                                   "x64_two_waves_depth4", "desc_lean", "desc_lean_no_nt"],
+                                   "x64_two_waves_depth4"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):
@@ -97,7 +95,7 @@ def test_variant_mixed_desc(tuned, algo):
     assert int(fb.cpu().numpy().view(np.uint64)[0]) == 3
 
 
-@pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "desc_lean"], indirect=True)
+@pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block"], indirect=True)
 @pytest.mark.parametrize("mode", ["digest", "validate", "stamp"])
 def test_desc_mixed_with_leftovers(tuned, mode):
     """XXH3 descriptor batches of every shape class: 4-16 KiB pages and
@@ -156,7 +154,7 @@ def test_desc_mixed_with_leftovers(tuned, mode):
 
 def test_retired_tuning_keys_fail():
     """Keys of the variants retired in round 2 are refused, and read -1."""
-    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 22, 99):
+    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 22, 99):
         assert pcs.get_tuning(k) == -1
         with pytest.raises(pcs.PcsError):
             pcs.set_tuning(k, 1)
