@@ -228,12 +228,20 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                   unsigned long long* first_bad) {
+    __shared__ uint64_t tile_h[16];
+    __shared__ uint8_t tile_st[16];  // 0 bad, 1 good, 2 not this kernel's page
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
+    // results staged per tile: one coalesced store per tile instead of 16
+    // scattered 8-byte (1-byte) stores inside the read stream, +1.0-1.7 % on
+    // config 3 (profiles/r02/desc_staged_lab.txt); stamps write headers
+    constexpr bool staged = MODE != kStamp;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
         const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        const uint64_t pg = t * 16 + (threadIdx.x >> 4);
+        const int grp = threadIdx.x >> 4;
+        const uint64_t pg = t * 16 + grp;
+        uint8_t st = 2;
         if (pg < n) {
             const uint64_t o = off[pg];
             const uint32_t P = len[pg];
@@ -241,8 +249,31 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                 const uint8_t* page = base + o;
                 uint64_t stored = 0;
                 const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
-                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+                if (!staged) {
+                    if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+                } else {
+                    st = h == stored ? 1 : 0;
+                    if (L.g == 0) tile_h[grp] = h;
+                }
             }
+        }
+        if (staged) {
+            if (L.g == 0) tile_st[grp] = st;
+            __syncthreads();
+            const uint64_t i = t * 16 + threadIdx.x;
+            const int s = threadIdx.x < 16 && i < n ? tile_st[threadIdx.x] : 2;
+            if (s != 2) {
+                if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
+                if (MODE == kValidate) st_nt(ok + i, (uint8_t)s);
+            }
+            if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+                for (int k = 0; k < 16 && t * 16 + k < n; ++k)
+                    if (tile_st[k] == 0) {
+                        note_bad(first_bad, t * 16 + k);
+                        break;
+                    }
+            }
+            __syncthreads();
         }
     }
 }
