@@ -594,11 +594,6 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
     }
 }
 
-
-__device__ __forceinline__ bool xxh64_fast_ok(uint64_t off, uint32_t P) {
-    return (P % 8u) == 0 && P >= 40u && (off % 8u) == 0;
-}
-
 // Pages off the 64-byte-piece shape (P % 64 != 0 or 8-byte-aligned only): one
 // quad per page, lane a reading accumulator a's words (xxh64_page).  The quad
 // layout for line-shaped pages (each quad loading its own 64 B pieces, 80 % of
@@ -614,28 +609,6 @@ __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict_
         const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 64 + (threadIdx.x >> 2);
         if (pg >= n) continue;
         const uint8_t* page = pages + pg * (uint64_t)P;
-        uint64_t stored = 0;
-        const uint64_t h = xxh64_page<false>(page, P, a, stored);
-        if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
-    }
-}
-
-// Descriptor pages k_xxh64_lds leaves (fast XXH64 shape, not line-shaped).
-template <int MODE>
-__global__ __launch_bounds__(256) void k_xxh64_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                                   const uint32_t* __restrict__ len, uint64_t n,
-                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   unsigned long long* first_bad) {
-    const int a = threadIdx.x & 3;
-    const uint64_t ntiles = (n + 63) / 64;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t pg = (remap ? xcd_tile(t0, ntiles) : t0) * 64 + (threadIdx.x >> 2);
-        if (pg >= n) continue;
-        const uint64_t o = off[pg];
-        const uint32_t P = len[pg];
-        if (!xxh64_fast_ok(o, P) || xxh64_lines_ok(o, P)) continue;
-        const uint8_t* page = base + o;
         uint64_t stored = 0;
         const uint64_t h = xxh64_page<false>(page, P, a, stored);
         if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
@@ -799,7 +772,7 @@ __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict_
                                                      uint8_t* __restrict__ ok, unsigned long long* first_bad) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (filter == 1 && (algo == 0 ? xxh3_fast_ok(off[i], len[i]) : xxh64_fast_ok(off[i], len[i]))) continue;
+        if (filter == 1 && (algo == 0 ? xxh3_fast_ok(off[i], len[i]) : xxh64_lines_ok(off[i], len[i]))) continue;
         if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
         generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
     }
@@ -1588,12 +1561,10 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             const unsigned grid = page_grid(n, kBlock / 4, 2);
             if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
             else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
-            // Pages off the line shape (usually none) go to the quad kernel: a
-            // capped grid-stride pass over the descriptors instead of one
-            // workgroup per 64 pages (14.8 -> ~4 us on config 3,
-            // profiles/r01/desc_passes.txt).
-            const unsigned qgrid = grid_for(n, kBlock / 4, kBlocksPerCu);
-            hipLaunchKernelGGL((k_xxh64_desc<MODE>), dim3(qgrid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb);
+            // Pages off the line shape (usually none) are left to the generic
+            // lanes below.  A separate quad-per-page pass over the
+            // descriptors for them cost 9.7 us per call on config 3 even when
+            // it found nothing to do (profiles/r02a_sweep.json).
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
