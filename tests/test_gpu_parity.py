@@ -183,6 +183,18 @@ def test_desc_odd_shapes(algo):
     ok, fb = pcs.desc_validate(base, d_off, d_len, len(lens), algo)
     okh = ok.cpu().numpy()
     assert okh[lens < 8].sum() == 0  # header-less pages never validate
+    # stamp at unaligned offsets (two-pass: digests, then k_scatter_stamp_desc):
+    # headers of pages >= 8 bytes get the digest, shorter pages stay untouched
+    pcs.desc_stamp(base, d_off, d_len, len(lens), algo)
+    h2 = base.cpu().numpy()
+    for o, L, w in zip(offs, lens, want):
+        o, L = int(o), int(L)
+        if L >= 8:
+            assert h2[o:o + 8].tobytes() == int(w).to_bytes(8, "little")
+        hdr = 8 if L >= 8 else 0
+        assert np.array_equal(h2[o + hdr:o + L], host[o + hdr:o + L])
+    ok, fb = pcs.desc_validate(base, d_off, d_len, len(lens), algo)
+    assert np.array_equal(ok.cpu().numpy().astype(bool), lens >= 8)
 
 
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
