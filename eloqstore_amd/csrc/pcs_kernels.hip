@@ -198,8 +198,10 @@ __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ 
     }
 }
 
-// Fixed stride, run-time page size.
-template <int MODE, bool NT, bool B4>
+// Fixed stride, run-time page size.  BODY 0 / 1: the chunked body one block
+// or four blocks per step (P % 256 == 0, 16-byte-aligned pages); BODY 2: the
+// any-size body (any P >= 249, any alignment).
+template <int MODE, bool NT, int BODY>
 __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                     uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                     unsigned long long* first_bad) {
@@ -211,13 +213,18 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
         if (pg >= n) continue;
         const uint8_t* page = pages + pg * (uint64_t)P;
         uint64_t stored = 0;
-        const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
+        const uint64_t h = BODY == 2   ? xxh3_page_any<NT>(page, P, L, stored)
+                           : BODY == 1 ? xxh3_page_rt4<NT>(page, P, L, stored)
+                                       : xxh3_page_rt<NT>(page, P, L, stored);
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
 }
 
 // Descriptor batch (mixed sizes), one group per page.  Pages that miss the
-// fast-path shape are left to k_generic_desc.  Measured alternatives, all
+// fast-path shape are left to k_generic_desc.  Handling the other long-path
+// pages here too (xxh3_page_any) cost config 3 1.2 % (152 against 136 VGPRs,
+// profiles/r02/desc_any_lab.txt), so they go to the generic pass, which
+// hashes them a group per page.  Measured alternatives, all
 // bit-exact and all slower on config 3: 4 KiB slices dealt
 // to the groups in rounds (-8 %), byte-budget slice windows (-12..-30 %),
 // per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %);
@@ -763,18 +770,52 @@ __device__ __forceinline__ void generic_one(const uint8_t* __restrict__ base, co
 }
 
 // One lane per range.  SKIP = 8 applies the page convention (hash [8, len),
-// stored digest in [0, 8)); SKIP = 0 hashes the raw range.  With FILTER set,
-// ranges the fast kernels handle are skipped.
+// stored digest in [0, 8)); SKIP = 0 hashes the raw range.  FILTER 1 (page
+// convention, seed 0, after the descriptor fast kernels): pages those kernels
+// took are skipped, and for XXH3 the other long-path pages (P >= 249: off the
+// 256-byte grid or unaligned) are hashed a 16-lane group per page with the
+// any-size body -- each wave ballots its lanes' such pages and works through
+// them four at a time.  FILTER 2: raw ranges k_xxh3_long took are skipped.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ len, uint64_t n, int algo,
                                                      uint64_t seed, int skip, int filter, uint64_t* __restrict__ out,
                                                      uint8_t* __restrict__ ok, unsigned long long* first_bad) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (filter == 1 && (algo == 0 ? xxh3_fast_ok(off[i], len[i]) : xxh64_lines_ok(off[i], len[i]))) continue;
-        if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
-        generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
+    const bool groups = filter == 1 && algo == 0;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform trip count, so the ballot below sees the whole wave
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
+        const uint64_t i = i0 + lane;
+        bool grp = false;
+        if (i < n) {
+            const uint64_t o = off[i];
+            const uint32_t P = len[i];
+            if (filter == 2 && xxh3_long_ok(base + o, P)) {
+            } else if (filter == 1 && algo == 0 && xxh3_fast_ok(o, P)) {
+            } else if (filter == 1 && algo == 0 && xxh3_group_ok(P)) {
+                grp = true;
+            } else if (filter == 1 && algo == 1 && xxh64_lines_ok(o, P)) {
+            } else {
+                generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
+            }
+        }
+        if (!groups) continue;
+        uint64_t mask = __ballot(grp);
+        if (!mask) continue;
+        const Xxh3Lane L = make_xxh3_lane(lane & 15);
+        while (mask) {  // wave-uniform
+            uint64_t m = mask;
+            for (int k = 0; k < (lane >> 4); ++k) m &= m - 1;  // this group's page: the (lane / 16)-th set bit
+            if (m) {
+                const uint64_t pg = i0 + (uint64_t)(__builtin_ctzll(m));
+                const uint8_t* page = base + off[pg];
+                uint64_t stored = 0;
+                const uint64_t h = xxh3_page_any<true>(page, len[pg], L, stored);
+                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+            }
+            for (int k = 0; k < 4; ++k) mask &= mask - 1;
+        }
     }
 }
 
@@ -1108,7 +1149,10 @@ __global__ void k_flip_byte(uint8_t* pages, uint64_t P, uint64_t n, uint64_t eve
 __global__ __launch_bounds__(256) void k_scatter_stamp(uint8_t* __restrict__ pages, uint64_t P, uint64_t n,
                                                       const uint64_t* __restrict__ dig) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) st_nt(reinterpret_cast<uint64_t*>(pages + i * P), dig[i]);
+    if (i >= n) return;
+    uint8_t* p = pages + i * P;
+    if (((uintptr_t)p & 7) == 0) st_nt(reinterpret_cast<uint64_t*>(p), dig[i]);
+    else __builtin_memcpy(p, &dig[i], 8);  // odd page sizes / unaligned batches
 }
 
 // descriptor form of the header pass: page i at base + off[i], len[i] bytes
@@ -1402,6 +1446,19 @@ template <int MODE, bool NT>
 hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
                              unsigned long long* fb, hipStream_t s) {
     const unsigned grid = page_grid(n, kBlock / 16, 1, P);  // kBlock/16 = one 16-page tile per block
+    if (P % 256 != 0) {  // off the chunk grid: the any-size body
+        hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, 2>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok,
+                           fb);
+        return hipGetLastError();
+    }
+    if ((uintptr_t)pages % 16 != 0) {
+        // on the grid but not 16-byte aligned: the chunked run-time-size body
+        // reads unaligned 16-byte pieces at ~6 TB/s (4 KiB pages at base + 8),
+        // the any-size body's 8-byte final-block loads at ~4.5
+        hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, 1>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok,
+                           fb);
+        return hipGetLastError();
+    }
     if (split_pages(P)) {
         const uint64_t ppb = 16 / (P / 4096);
         const uint64_t need = (n + ppb - 1) / ppb;
@@ -1423,10 +1480,10 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
 #undef CASE
         default:
             if (rt_batch4())
-                hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, true>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
+                hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, 1>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
                                    n, out, ok, fb);
             else
-                hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, false>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
+                hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, 0>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P,
                                    n, out, ok, fb);
     }
     return hipGetLastError();
@@ -1441,7 +1498,9 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
     if (n == 0) return hipSuccess;
     const bool aligned16 = ((uintptr_t)pages % 16) == 0;
     const bool aligned8 = ((uintptr_t)pages % 8) == 0;
-    if (algo == 0 && aligned16 && P % 256 == 0 && P >= 256 && P <= 0xFFFFFFFFull) {
+    // XXH3: the chunked kernels on the 256-byte grid at 16-byte alignment, the
+    // any-size body (k_xxh3_stride<..., 2>) for every other long-path size
+    if (algo == 0 && P >= 249 && P <= 0xFFFFFFFFull) {
         if constexpr (MODE == kStamp) {
             // two-pass stamp: digests into a compact array (the fast digest
             // kernel), then one scattered 8-byte write per page

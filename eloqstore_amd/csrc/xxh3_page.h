@@ -311,6 +311,94 @@ __device__ __forceinline__ bool xxh3_fast_ok(uint64_t off, uint32_t P) {
     return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
 }
 
+// 8-byte load at any alignment (global_load_dwordx2; the part reads unaligned
+// addresses in hardware)
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+
+// The final (partial) block of an input of any length len > 240 at any
+// alignment (xxhash.h:6005-6016), for page sizes off the 256-byte chunk grid.
+// Lane g takes accumulator lane l = 2(g & 3) + ((g >> 2) & 1) of stripes
+// g >> 3, (g >> 3) + 2, ... (8-byte loads; each group instruction reads 128
+// contiguous bytes), lanes 0-7 also the last stripe (secret + 121).  A lane's
+// multiply terms belong to acc[l] and its raw words to acc[l ^ 1], both of
+// pair g & 3, so the pair sums fold over lanes g = p (mod 4) exactly like the
+// block sums.  Every lane of the group must be active.
+__device__ __forceinline__ void xxh3_final_any(const uint8_t* in, uint32_t len, int NB, const Xxh3Lane& L,
+                                               uint64_t& Te, uint64_t& To) {
+    const int g = L.g;
+    const bool odd = (g >> 2) & 1;
+    const int l = 2 * (g & 3) + (int)odd;
+    const int nbS = (int)((len - 1u - 1024u * (uint32_t)NB) / 64u);  // ordinary stripes, 0..15
+    const uint8_t* blk = in + 1024u * (uint32_t)NB + 8 * l;
+    uint64_t M = 0, R = 0;
+    for (int s = g >> 3; s < nbS; s += 2) {
+        const uint64_t v = ld64u(blk + 64 * s);
+        M += mul32x32(v ^ c_keys.acc[s + l]);
+        R += v;
+    }
+    if (g < 8) {
+        const uint64_t v = ld64u(in + len - 64 + 8 * l);
+        M += mul32x32(v ^ c_keys.last[l]);
+        R += v;
+    }
+    Te = odd ? R : M;
+    To = odd ? M : R;
+    Te += dpp64<kRowRor4>(Te);
+    To += dpp64<kRowRor4>(To);
+    Te += dpp64<kRowRor8>(Te);
+    To += dpp64<kRowRor8>(To);
+}
+
+// Any page size P >= 249 (hashed length > 240, the long path), any alignment:
+// the full 1 KiB blocks as in xxh3_page_rt4 (16-byte lane loads, batches of
+// four), the final block by xxh3_final_any.  The last full block's carry
+// word (page word 128 NB) is read on its own, so no load crosses the page end.
+template <bool NT>
+__device__ __forceinline__ uint64_t xxh3_page_any(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
+                                                  uint64_t& stored) {
+    const int NB = (int)((P - 9) / 1024);
+    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
+    uint64_t Ae = L.init_e, Ao = L.init_o;
+    stored = ld64u(page);
+    const uint64_t carry_last = NB > 0 ? ld64u(page + 1024u * (uint32_t)NB) : 0;
+    u32x4 head = {0, 0, 0, 0};
+    if (NB > 0) head = ld16<NT>(base);
+    for (int b0 = 0; b0 < NB; b0 += 4) {
+        u32x4 d[5][4];
+        d[0][0] = head;
+#pragma unroll
+        for (int i = 0; i <= 4; ++i) {
+            const int b = b0 + i;
+            const int nc = (b >= NB) ? 0 : (i == 4) ? 1 : 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < nc && !(i == 0 && c == 0)) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int b = b0 + i;
+            if (b < NB) {
+                const uint64_t carry = (b + 1 == NB) ? carry_last : lo64(d[i + 1][0]);
+                uint64_t Te, To;
+                xxh3_block_terms<false>(L, d[i], carry, 4, Te, To);
+                Ae = xxh3_scramble(Ae + Te, L.ks_e);
+                Ao = xxh3_scramble(Ao + To, L.ks_o);
+            }
+        }
+        head = d[4][0];
+    }
+    uint64_t Te, To;
+    xxh3_final_any(page + 8, P - 8, NB, L, Te, To);
+    return xxh3_merge(L, Ae + Te, Ao + To, (uint64_t)(P - 8));
+}
+
+// pages the group kernels take at all: the XXH3 long path (hashed length > 240)
+__device__ __forceinline__ bool xxh3_group_ok(uint32_t P) { return P >= 249u; }
+
 // Tile t of nb -> renumbered so that the blocks of one XCD (blockIdx % 8)
 // walk one contiguous eighth of the batch (cdna_hip_programming.md T1,
 // bijective form).

@@ -85,10 +85,12 @@ int pcs_set_device(int device);
 int pcs_synchronize(pcs_stream_t stream);
 
 /* ---- device-resident, fixed page size (pages contiguous, stride page_size) --
- * Fast paths: XXH3 needs a 16-byte-aligned base and page_size % 256 == 0
- * (every legal EloqStore data_page_size of 1-32 KiB and 64 KiB chunks);
- * XXH64 needs an 8-byte-aligned base, page_size % 8 == 0 and page_size >= 40.
- * Any other shape is still computed exactly (generic kernel), only slower. */
+ * Fast paths: XXH3 runs a 16-lane group per page for every page size of its
+ * long path (page_size >= 249) at any alignment; fastest at page_size % 256
+ * == 0 on a 16-byte-aligned base (every power-of-two data_page_size and 64 KiB
+ * chunks), 4-7 TB/s for other sizes.  XXH64 needs an
+ * 8-byte-aligned base, page_size % 8 == 0 and page_size >= 40.  Any other
+ * shape is still computed exactly (generic kernel), only slower. */
 
 /* d_digests[i] = digest of page i over [8, page_size). */
 int pcs_pages_digest_dev(const void *d_pages, uint64_t page_size, uint64_t n_pages, int algo,

@@ -577,6 +577,43 @@ def test_cpp_dropin_program():
     assert r.returncode == 0 and "dropin ok" in r.stdout, r.stdout + r.stderr
 
 
+ANY_SIZES = [249, 250, 255, 257, 1000, 1032, 1033, 1039, 1040, 1096, 2047, 2049, 4000, 4095, 4097, 4104, 4160, 5000,
+             8000, 12345, 16000, 65535]
+
+
+@pytest.mark.parametrize("P", ANY_SIZES)
+@pytest.mark.parametrize("shift", [0, 8, 3])
+def test_xxh3_any_page_size(P, shift):
+    """XXH3 pages off the 256-byte grid and at any alignment (the any-size
+    group body, xxh3_page_any: full blocks by 16-byte lane loads, the final
+    block by 8-byte stripe loads), through the fixed-stride and the
+    descriptor entry points, digest / validate / stamp.  Sizes cover every
+    final-block shape: 0..15 ordinary stripes, NB = 0 (P < 1033), the last
+    stripe across a chunk edge, EloqStore's largest data_page_size (65535).
+    The batch ends at the end of its buffer."""
+    rng = np.random.default_rng(P * 8 + shift)
+    n = 19 if P < 20000 else 5
+    host = rng.integers(0, 256, size=n * P, dtype=np.uint8)
+    want = oracle.pages_digest(host, P, pcs.XXH3_64)
+    buf = torch.empty(n * P + shift, dtype=torch.uint8, device=DEV)
+    buf[shift:] = torch.from_numpy(host).to(DEV)
+    pages = buf[shift:]
+    assert np.array_equal(u64(pcs.pages_digest(pages, P, n, pcs.XXH3_64)), want)
+    offs = (np.arange(n, dtype=np.uint64) * np.uint64(P) + np.uint64(shift)).view(np.int64)
+    d_off = torch.from_numpy(offs).to(DEV)
+    d_len = torch.full((n,), P, dtype=torch.int32, device=DEV)
+    assert np.array_equal(u64(pcs.desc_digest(buf, d_off, d_len, n, pcs.XXH3_64)), want)
+    pcs.pages_stamp(pages, P, n, pcs.XXH3_64)
+    h2 = pages.cpu().numpy()
+    for i in range(n):
+        assert h2[i * P:i * P + 8].tobytes() == int(want[i]).to_bytes(8, "little")
+    ok, fb = pcs.desc_validate(buf, d_off, d_len, n, pcs.XXH3_64)
+    assert ok.cpu().numpy().all()
+    pcs.flip_byte(pages, P, n, every=4, byte_offset=P - 1)  # the page's last byte: the last stripe
+    ok, fb = pcs.pages_validate(pages, P, n, pcs.XXH3_64)
+    assert list(np.flatnonzero(ok.cpu().numpy() == 0)) == list(range(0, n, 4)) and int(u64(fb)[0]) == 0
+
+
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 @pytest.mark.parametrize("shift", [1, 8, 24])
 def test_unaligned_page_base(algo, shift):
