@@ -319,34 +319,45 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
     return v;
 }
 
-// The final (partial) block of an input of any length len > 240 at any
-// alignment (xxhash.h:6005-6016), for page sizes off the 256-byte chunk grid.
-// Lane g takes accumulator lane l = 2(g & 3) + ((g >> 2) & 1) of stripes
-// g >> 3, (g >> 3) + 2, ... (8-byte loads; each group instruction reads 128
-// contiguous bytes), lanes 0-7 also the last stripe (secret + 121).  A lane's
-// multiply terms belong to acc[l] and its raw words to acc[l ^ 1], both of
-// pair g & 3, so the pair sums fold over lanes g = p (mod 4) exactly like the
-// block sums.  Every lane of the group must be active.
-__device__ __forceinline__ void xxh3_final_any(const uint8_t* in, uint32_t len, int NB, const Xxh3Lane& L,
-                                               uint64_t& Te, uint64_t& To) {
+// The final (partial) block for any page size P >= 249 (xxhash.h:6005-6016).
+// Input word j of the block (page word 128 NB + 1 + j) is in an ordinary
+// stripe iff j < 8 nbS, nbS = (P - 9 - 1024 NB) / 64; with the chunk layout
+// of the full blocks (lane g, chunk c holds 16-byte piece k = 16c + g, words
+// j = 2k - 1 and 2k), piece k < kmax = 4 nbS is used whole and piece kmax for
+// its low word only (so it is loaded as 8 bytes: no load crosses the page
+// end).  The last stripe (page bytes [P - 64, P), secret + 121) need not sit
+// on the piece grid, so lanes 0-7 load its words separately (lastw): lane g
+// holds last-stripe lane l = 2(g & 3) + (g >> 2), whose multiply term goes to
+// acc[l] and raw word to acc[l ^ 1], both of pair g & 3, i.e. into this
+// lane's V sums.  For P % 256 == 0 this is exactly xxh3_block_terms<true>.
+__device__ __forceinline__ void xxh3_final_terms(const Xxh3Lane& L, const u32x4 (&d)[4], int kmax, uint64_t lastw,
+                                                 uint64_t& Te, uint64_t& To) {
+    uint64_t Ue = 0, Uo = 0, Ve = 0, Vo = 0;
     const int g = L.g;
-    const bool odd = (g >> 2) & 1;
-    const int l = 2 * (g & 3) + (int)odd;
-    const int nbS = (int)((len - 1u - 1024u * (uint32_t)NB) / 64u);  // ordinary stripes, 0..15
-    const uint8_t* blk = in + 1024u * (uint32_t)NB + 8 * l;
-    uint64_t M = 0, R = 0;
-    for (int s = g >> 3; s < nbS; s += 2) {
-        const uint64_t v = ld64u(blk + 64 * s);
-        M += mul32x32(v ^ c_keys.acc[s + l]);
-        R += v;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = 16 * c + g;
+        const uint64_t w0 = lo64(d[c]), w1 = hi64(d[c]);
+        const bool use0 = k <= kmax && k != 0;  // piece 0's low word is the previous block's carry
+        const bool use1 = k < kmax;
+        const uint64_t m0 = mul32x32(w0 ^ L.k[c][0]);
+        const uint64_t m1 = mul32x32(w1 ^ L.k[c][1]);
+        Uo += use0 ? m0 : 0;
+        Ue += use0 ? w0 : 0;
+        Ve += use1 ? m1 : 0;
+        Vo += use1 ? w1 : 0;
     }
     if (g < 8) {
-        const uint64_t v = ld64u(in + len - 64 + 8 * l);
-        M += mul32x32(v ^ c_keys.last[l]);
-        R += v;
+        if (g < 4) {
+            Ve += mul32x32(lastw ^ L.kl0);
+            Vo += lastw;
+        } else {
+            Vo += mul32x32(lastw ^ L.kl1);
+            Ve += lastw;
+        }
     }
-    Te = odd ? R : M;
-    To = odd ? M : R;
+    Te = Ve + dpp64<kRowRor15>(Ue);
+    To = Vo + dpp64<kRowRor15>(Uo);
     Te += dpp64<kRowRor4>(Te);
     To += dpp64<kRowRor4>(To);
     Te += dpp64<kRowRor8>(Te);
@@ -354,46 +365,65 @@ __device__ __forceinline__ void xxh3_final_any(const uint8_t* in, uint32_t len, 
 }
 
 // Any page size P >= 249 (hashed length > 240, the long path), any alignment:
-// the full 1 KiB blocks as in xxh3_page_rt4 (16-byte lane loads, batches of
-// four), the final block by xxh3_final_any.  The last full block's carry
-// word (page word 128 NB) is read on its own, so no load crosses the page end.
+// xxh3_page_rt4's batches of four 1 KiB blocks, the final block's pieces
+// loaded in the same batch as the blocks before it (predicated per lane: only
+// pieces holding ordinary-stripe words), its terms by xxh3_final_terms.
 template <bool NT>
 __device__ __forceinline__ uint64_t xxh3_page_any(const uint8_t* __restrict__ page, uint32_t P, const Xxh3Lane& L,
                                                   uint64_t& stored) {
     const int NB = (int)((P - 9) / 1024);
-    const u32x4* base = reinterpret_cast<const u32x4*>(page) + L.g;
-    uint64_t Ae = L.init_e, Ao = L.init_o;
+    const int kmax = 4 * (int)((P - 9 - 1024u * (uint32_t)NB) / 64u);  // 0..60
+    const int TB = NB + 1;
+    const int g = L.g;
+    const u32x4* base = reinterpret_cast<const u32x4*>(page) + g;
+    const uint64_t lastw = g < 8 ? ld64u(page + P - 64 + 8 * (2 * (g & 3) + (g >> 2))) : 0;
     stored = ld64u(page);
-    const uint64_t carry_last = NB > 0 ? ld64u(page + 1024u * (uint32_t)NB) : 0;
-    u32x4 head = {0, 0, 0, 0};
-    if (NB > 0) head = ld16<NT>(base);
-    for (int b0 = 0; b0 < NB; b0 += 4) {
+    uint64_t Ae = L.init_e, Ao = L.init_o;
+    // piece c of the final block for this lane: whole, low word only, or none
+    auto final_piece = [&](int c) -> u32x4 {
+        const int k = 16 * c + g;
+        const u32x4* q = base + NB * 64 + c * 16;
+        if (k < kmax) return ld16<NT>(q);
+        u32x4 v = {0, 0, 0, 0};
+        if (k == kmax) {
+            const uint64_t w = ld64u(reinterpret_cast<const uint8_t*>(q));
+            v.x = (uint32_t)w;
+            v.y = (uint32_t)(w >> 32);
+        }
+        return v;
+    };
+    u32x4 head = NB > 0 ? ld16<NT>(base) : final_piece(0);
+    for (int b0 = 0; b0 < TB; b0 += 4) {
         u32x4 d[5][4];
         d[0][0] = head;
 #pragma unroll
         for (int i = 0; i <= 4; ++i) {
             const int b = b0 + i;
-            const int nc = (b >= NB) ? 0 : (i == 4) ? 1 : 4;
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c < nc && !(i == 0 && c == 0)) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
+            for (int c = 0; c < 4; ++c) {
+                if (i == 0 && c == 0) continue;
+                if (b < NB && (i < 4 || c == 0)) d[i][c] = ld16<NT>(base + b * 64 + c * 16);
+                else if (b == NB && (i < 4 || c == 0)) d[i][c] = final_piece(c);
+                else d[i][c] = u32x4{0, 0, 0, 0};
+            }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int b = b0 + i;
+            uint64_t Te, To;
             if (b < NB) {
-                const uint64_t carry = (b + 1 == NB) ? carry_last : lo64(d[i + 1][0]);
-                uint64_t Te, To;
-                xxh3_block_terms<false>(L, d[i], carry, 4, Te, To);
+                xxh3_block_terms<false>(L, d[i], lo64(d[i + 1][0]), 4, Te, To);
                 Ae = xxh3_scramble(Ae + Te, L.ks_e);
                 Ao = xxh3_scramble(Ao + To, L.ks_o);
+            } else if (b == NB) {
+                xxh3_final_terms(L, d[i], kmax, lastw, Te, To);
+                Ae += Te;
+                Ao += To;
             }
         }
         head = d[4][0];
     }
-    uint64_t Te, To;
-    xxh3_final_any(page + 8, P - 8, NB, L, Te, To);
-    return xxh3_merge(L, Ae + Te, Ao + To, (uint64_t)(P - 8));
+    return xxh3_merge(L, Ae, Ao, (uint64_t)(P - 8));
 }
 
 // pages the group kernels take at all: the XXH3 long path (hashed length > 240)

@@ -88,7 +88,7 @@ int pcs_synchronize(pcs_stream_t stream);
  * Fast paths: XXH3 runs a 16-lane group per page for every page size of its
  * long path (page_size >= 249) at any alignment; fastest at page_size % 256
  * == 0 on a 16-byte-aligned base (every power-of-two data_page_size and 64 KiB
- * chunks), 4-7 TB/s for other sizes.  XXH64 needs an
+ * chunks), 5-7 TB/s for other sizes.  XXH64 needs an
  * 8-byte-aligned base, page_size % 8 == 0 and page_size >= 40.  Any other
  * shape is still computed exactly (generic kernel), only slower. */
 
