@@ -230,6 +230,11 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
 // per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %);
 // round 2 (commit 99804f2): pages dealt to a wave's groups as they free up
 // (+-1 %), a wave's pages as a stream of adjacent 4 KiB slices (-5..-8 %).
+// One workgroup per tile, grid = tiles (no grid-stride loop): 125 VGPRs and
+// 4 waves per SIMD, against 136 and 3 for the same body inside a grid-stride
+// loop: +1.1 % digest / +0.8 % validate on config 3
+// (profiles/r02/desc_tp_lab.txt, list 1 vs 0).  Loading the next tile's
+// descriptors ahead with 2 or 4 tiles per workgroup was slower (-0.4..-2.7 %).
 template <int MODE, bool NT, bool B4>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
@@ -239,48 +244,44 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
     __shared__ uint8_t tile_st[16];  // 0 bad, 1 good, 2 not this kernel's page
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
-    const bool remap = gridDim.x == ntiles;
+    const uint64_t t = xcd_tile(blockIdx.x, ntiles);  // the launch covers every tile once
     // results staged per tile: one coalesced store per tile instead of 16
     // scattered 8-byte (1-byte) stores inside the read stream, +1.0-1.7 % on
     // config 3 (profiles/r02/desc_staged_lab.txt); stamps write headers
     constexpr bool staged = MODE != kStamp;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
-        const int grp = threadIdx.x >> 4;
-        const uint64_t pg = t * 16 + grp;
-        uint8_t st = 2;
-        if (pg < n) {
-            const uint64_t o = off[pg];
-            const uint32_t P = len[pg];
-            if (xxh3_fast_ok(o, P)) {
-                const uint8_t* page = base + o;
-                uint64_t stored = 0;
-                const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
-                if (!staged) {
-                    if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
-                } else {
-                    st = h == stored ? 1 : 0;
-                    if (L.g == 0) tile_h[grp] = h;
-                }
+    const int grp = threadIdx.x >> 4;
+    const uint64_t pg = t * 16 + grp;
+    uint8_t st = 2;
+    if (pg < n) {
+        const uint64_t o = off[pg];
+        const uint32_t P = len[pg];
+        if (xxh3_fast_ok(o, P)) {
+            const uint8_t* page = base + o;
+            uint64_t stored = 0;
+            const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
+            if (!staged) {
+                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+            } else {
+                st = h == stored ? 1 : 0;
+                if (L.g == 0) tile_h[grp] = h;
             }
         }
-        if (staged) {
-            if (L.g == 0) tile_st[grp] = st;
-            __syncthreads();
-            const uint64_t i = t * 16 + threadIdx.x;
-            const int s = threadIdx.x < 16 && i < n ? tile_st[threadIdx.x] : 2;
-            if (s != 2) {
-                if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
-                if (MODE == kValidate) st_nt(ok + i, (uint8_t)s);
-            }
-            if (MODE == kValidate && first_bad && threadIdx.x == 0) {
-                for (int k = 0; k < 16 && t * 16 + k < n; ++k)
-                    if (tile_st[k] == 0) {
-                        note_bad(first_bad, t * 16 + k);
-                        break;
-                    }
-            }
-            __syncthreads();
+    }
+    if (staged) {
+        if (L.g == 0) tile_st[grp] = st;
+        __syncthreads();
+        const uint64_t i = t * 16 + threadIdx.x;
+        const int s = threadIdx.x < 16 && i < n ? tile_st[threadIdx.x] : 2;
+        if (s != 2) {
+            if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
+            if (MODE == kValidate) st_nt(ok + i, (uint8_t)s);
+        }
+        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+            for (int k = 0; k < 16 && t * 16 + k < n; ++k)
+                if (tile_st[k] == 0) {
+                    note_bad(first_bad, t * 16 + k);
+                    break;
+                }
         }
     }
 }
@@ -1605,7 +1606,10 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
     if (skip == 8 && seed == 0) {
         // fast kernels for conforming pages, generic lanes for the rest
         if (algo == 0) {
-            const unsigned grid = page_grid(n, kBlock / 16, 1);
+            // one workgroup per 16-page tile, every tile covered once
+            const uint64_t ntiles = (n + 15) / 16;
+            if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+            const unsigned grid = (unsigned)ntiles;
 #define L(NT_, B4_) \
     hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
             if (use_nt()) {
