@@ -46,7 +46,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--algo", type=int, default=0)
+    ap.add_argument("--knob", type=int, default=None, help="tuning key to sweep per layout")
+    ap.add_argument("--values", default="0")
+    ap.add_argument("--layouts", default=None, help="comma-separated layout name prefixes to keep")
     args = ap.parse_args()
+    values = [int(v) for v in args.values.split(",")] if args.knob is not None else [None]
     torch.cuda.set_device(0)
     lens3 = mixed_sizes(SEED3, 0, N3).astype(np.uint64)
     total = int(lens3.sum())
@@ -68,6 +72,9 @@ def main():
         w = lens3[: (N3 // W) * W].reshape(-1, W)
         layouts[f"config 3 sorted in {W}"] = packed(np.sort(w, axis=1).reshape(-1))
     layouts["config 3 sorted"] = packed(srt)
+    if args.layouts:
+        keep = [k.strip() for k in args.layouts.split(",")]
+        layouts = {k: v for k, v in layouts.items() if any(k.startswith(p) for p in keep)}
     dev = {}
     for name, (offs, lens) in layouts.items():
         assert int(offs[-1]) + int(lens[-1]) <= total
@@ -88,8 +95,14 @@ def main():
     res = {}
     for r in range(args.rounds):
         for name, (d_off, d_len, n, nbytes) in dev.items():
-            t = timed(lambda: pcs.desc_digest(arena, d_off, d_len, n, args.algo, out=out))
-            res.setdefault(name, []).append((nbytes + 8 * n) / t / 8e12)
+            for v in values:
+                if v is not None:
+                    pcs.set_tuning(args.knob, v)
+                t = timed(lambda: pcs.desc_digest(arena, d_off, d_len, n, args.algo, out=out))
+                key = name if v is None else f"{name} [{args.knob}={v}]"
+                res.setdefault(key, []).append((nbytes + 8 * n) / t / 8e12)
+            if args.knob is not None:
+                pcs.set_tuning(args.knob, values[0])
         for P in (4096, 16384):
             n = total // P
             t = timed(lambda: pcs.pages_digest(arena, P, n, args.algo, out=out))
