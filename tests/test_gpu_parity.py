@@ -294,7 +294,7 @@ def test_host_single_page_api():
     assert int.from_bytes(short[:8], "little") == oracle.xxh3_64(bytes(short[8:]))
 
 
-@pytest.mark.parametrize("P", [4096, 8192, 1000])
+@pytest.mark.parametrize("P", [4096, 8192, 1000, 5000])
 def test_host_batch_api(P):
     n = 300
     pages = [bytearray(splitmix_words(5, i, P // 8).tobytes()) for i in range(n)]
