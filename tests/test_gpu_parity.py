@@ -360,6 +360,31 @@ def test_cli(tmp_path):
     assert r.returncode == 1 and "exceeds file size" in r.stderr
 
 
+@pytest.mark.parametrize("P", [4096, 5000])
+def test_cli_scan_windows(tmp_path, P):
+    """Whole-file scrub over several 64 MiB chunks (two batches in flight,
+    reads split over threads): every corrupted page is counted, the first
+    offset reported, a trailing partial page ignored; the same with small
+    chunks and one reader thread."""
+    f = tmp_path / "big.bin"
+    tool = pcs.TOOL_PATH
+    n = (300 << 20) // P + 3
+    r = subprocess.run([tool, "--gen", str(f), str(n), str(P), "0x5EED0009"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    with open(f, "r+b") as fh:
+        for pg in (n - 2, (260 << 20) // P, 7):  # second window, across the boundary region, first window
+            fh.seek(pg * P + P // 2)
+            b = fh.read(1)
+            fh.seek(pg * P + P // 2)
+            fh.write(bytes([b[0] ^ 0x20]))
+        fh.seek(0, 2)
+        fh.write(b"\x01" * (P // 3))  # partial trailing page
+    for env in (dict(os.environ), dict(os.environ, PCS_SCAN_THREADS="1", PCS_SCAN_CHUNK_MIB="5")):
+        r = subprocess.run([tool, "--scan", str(f), str(P)], capture_output=True, text=True, env=env)
+        assert r.returncode == 2, r.stdout + r.stderr
+        assert f"{n} pages of {P} bytes: 3 corrupted, first at offset {7 * P}" in r.stdout, r.stdout
+
+
 @pytest.mark.parametrize("P,n,algo", [
     (4096, 1 << 20, pcs.XXH3_64),    # BASELINE config 2 (fixed-size kernel)
     (16384, 1 << 18, pcs.XXH3_64),   # 16 KiB sweep (split-page kernel)

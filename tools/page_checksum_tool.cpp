@@ -140,9 +140,20 @@ bool pwrite_full(int fd, const char* buf, uint64_t len, uint64_t off) {
 
 // pread of one chunk split over a few threads: a single thread's copy out of
 // the page cache (~6 GiB/s) would otherwise bound the scrub.
+// PCS_SCAN_THREADS / PCS_SCAN_PIECE_MIB / PCS_SCAN_CHUNK_MIB override the
+// reader threads (8), the read piece (8 MiB) and the chunk per batch (64 MiB);
+// tools/lab/scan_lab.sh sweeps them (more threads or larger chunks measured no
+// faster, profiles/r02/scan_lab.txt).
+uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* v = std::getenv(name);
+    uint64_t x;
+    return v && parse_u64(v, x) && x > 0 ? x : dflt;
+}
+
 bool pread_parallel(int fd, char* buf, uint64_t len, uint64_t off) {
-    constexpr uint64_t kPiece = 8ull << 20;
-    const unsigned T = (unsigned)std::min<uint64_t>(8, (len + kPiece - 1) / kPiece);
+    static const uint64_t kThreads = env_u64("PCS_SCAN_THREADS", 8);
+    static const uint64_t kPiece = env_u64("PCS_SCAN_PIECE_MIB", 8) << 20;
+    const unsigned T = (unsigned)std::min<uint64_t>(kThreads, (len + kPiece - 1) / kPiece);
     if (T <= 1) return pread_full(fd, buf, len, off);
     std::vector<std::thread> th;
     std::vector<char> ok(T, 1);
@@ -172,7 +183,7 @@ int bulk(bool stamp, const char* path, const char* size_s) {
         std::fprintf(stderr, "File %s holds no whole page of %llu bytes\n", path, (unsigned long long)P);
         return 1;
     }
-    const uint64_t chunk = std::max<uint64_t>(1, (64ull << 20) / P);
+    const uint64_t chunk = std::max<uint64_t>(1, (env_u64("PCS_SCAN_CHUNK_MIB", 64) << 20) / P);
     void* buf[2] = {nullptr, nullptr};
     pcs_batch* batch[2] = {nullptr, nullptr};
     int rc = 0;
