@@ -220,72 +220,6 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
     }
 }
 
-// Descriptor batch (mixed sizes), one group per page.  Pages that miss the
-// fast-path shape are left to k_generic_desc.  Handling the other long-path
-// pages here too (xxh3_page_any) cost config 3 1.2 % (152 against 136 VGPRs,
-// profiles/r02/desc_any_lab.txt), so they go to the generic pass, which
-// hashes them a group per page.  Measured alternatives, all
-// bit-exact and all slower on config 3 (DESIGN.md §4.1a): 4 KiB slices dealt
-// to the groups in rounds (-8 %), byte-budget slice windows (-12..-30 %),
-// per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %);
-// round 2 (commit 99804f2): pages dealt to a wave's groups as they free up
-// (+-1 %), a wave's pages as a stream of adjacent 4 KiB slices (-5..-8 %).
-// One workgroup per tile, grid = tiles (no grid-stride loop): 125 VGPRs and
-// 4 waves per SIMD, against 136 and 3 for the same body inside a grid-stride
-// loop: +1.1 % digest / +0.8 % validate on config 3
-// (profiles/r02/desc_tp_lab.txt, list 1 vs 0).  Loading the next tile's
-// descriptors ahead with 2 or 4 tiles per workgroup was slower (-0.4..-2.7 %).
-template <int MODE, bool NT, bool B4>
-__global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ len, uint64_t n,
-                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  unsigned long long* first_bad) {
-    __shared__ uint64_t tile_h[16];
-    __shared__ uint8_t tile_st[16];  // 0 bad, 1 good, 2 not this kernel's page
-    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
-    const uint64_t ntiles = (n + 15) / 16;
-    const uint64_t t = xcd_tile(blockIdx.x, ntiles);  // the launch covers every tile once
-    // results staged per tile: one coalesced store per tile instead of 16
-    // scattered 8-byte (1-byte) stores inside the read stream, +1.0-1.7 % on
-    // config 3 (profiles/r02/desc_staged_lab.txt); stamps write headers
-    constexpr bool staged = MODE != kStamp;
-    const int grp = threadIdx.x >> 4;
-    const uint64_t pg = t * 16 + grp;
-    uint8_t st = 2;
-    if (pg < n) {
-        const uint64_t o = off[pg];
-        const uint32_t P = len[pg];
-        if (xxh3_fast_ok(o, P)) {
-            const uint8_t* page = base + o;
-            uint64_t stored = 0;
-            const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
-            if (!staged) {
-                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
-            } else {
-                st = h == stored ? 1 : 0;
-                if (L.g == 0) tile_h[grp] = h;
-            }
-        }
-    }
-    if (staged) {
-        if (L.g == 0) tile_st[grp] = st;
-        __syncthreads();
-        const uint64_t i = t * 16 + threadIdx.x;
-        const int s = threadIdx.x < 16 && i < n ? tile_st[threadIdx.x] : 2;
-        if (s != 2) {
-            if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
-            if (MODE == kValidate) st_nt(ok + i, (uint8_t)s);
-        }
-        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
-            for (int k = 0; k < 16 && t * 16 + k < n; ++k)
-                if (tile_st[k] == 0) {
-                    note_bad(first_bad, t * 16 + k);
-                    break;
-                }
-        }
-    }
-}
-
 // Page list: page pg is the absolute address ptrs[pg], all of size P
 // (P % 256 == 0, 16-byte aligned; checked by the caller).  Used for pool pages
 // in registered host memory, read in place over PCIe (zero-copy): the list
@@ -648,7 +582,8 @@ __device__ __forceinline__ uint64_t mix16(const uint8_t* in, uint64_t k0, uint64
     return mul_fold64(ld64(in) ^ k0, ld64(in + 8) ^ k1);
 }
 
-__device__ uint64_t xxh3_any(const uint8_t* in, uint64_t len) {
+// XXH3_64bits for len <= 240 (the short and mid-size classes)
+__device__ __forceinline__ uint64_t xxh3_short(const uint8_t* in, uint64_t len) {
     if (len <= 16) {  // XXH3_len_0to16_64b, :4696-4704
         if (len > 8) {
             const uint64_t lo = ld64(in) ^ (secret64(24) ^ secret64(32));
@@ -679,7 +614,7 @@ __device__ uint64_t xxh3_any(const uint8_t* in, uint64_t len) {
         }
         return xxh3_avalanche(acc);
     }
-    if (len <= 240) {  // XXH3_len_129to240_64b, :4802-4856
+    {  // XXH3_len_129to240_64b, :4802-4856 (len <= 240 here)
         uint64_t acc = len * kP64_1;
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc += mix16(in + 16 * i, secret64(16 * i), secret64(16 * i + 8));
@@ -693,6 +628,10 @@ __device__ uint64_t xxh3_any(const uint8_t* in, uint64_t len) {
         }
         return xxh3_avalanche(acc + tail);
     }
+}
+
+__device__ uint64_t xxh3_any(const uint8_t* in, uint64_t len) {
+    if (len <= 240) return xxh3_short(in, len);
     // long input, scalar (xxhash.h:5988-6081)
     uint64_t acc[8];
 #pragma unroll
@@ -770,53 +709,113 @@ __device__ __forceinline__ void generic_one(const uint8_t* __restrict__ base, co
     }
 }
 
+// Descriptor batch (mixed sizes), one group per page, every shape: pages on
+// the 256-byte chunk grid at 16-byte offsets take the chunked body, other
+// long-path pages (P >= 249) the any-size body, shorter ones one lane of the
+// group (xxh3_short).  So no generic pass follows.  (In the earlier
+// grid-stride form the any-size branch cost 1.2 %, 152 against 136 VGPRs,
+// profiles/r02/desc_any_lab.txt; one tile per workgroup compiles all three
+// branches in 126.)  Measured alternatives, all
+// bit-exact and all slower on config 3 (DESIGN.md §4.1a): 4 KiB slices dealt
+// to the groups in rounds (-8 %), byte-budget slice windows (-12..-30 %),
+// per-tile size sort (+-1 %), LPT page pairs (-2 %), a 128-VGPR cap (-0.3 %);
+// round 2 (commit 99804f2): pages dealt to a wave's groups as they free up
+// (+-1 %), a wave's pages as a stream of adjacent 4 KiB slices (-5..-8 %).
+// One workgroup per tile, grid = tiles (no grid-stride loop): 125 VGPRs and
+// 4 waves per SIMD, against 136 and 3 for the same body inside a grid-stride
+// loop: +1.1 % digest / +0.8 % validate on config 3
+// (profiles/r02/desc_tp_lab.txt, list 1 vs 0).  Loading the next tile's
+// descriptors ahead with 2 or 4 tiles per workgroup was slower (-0.4..-2.7 %).
+template <int MODE, bool NT, bool B4>
+__global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ len, uint64_t n,
+                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                  unsigned long long* first_bad) {
+    __shared__ uint64_t tile_h[16];
+    __shared__ uint8_t tile_st[16];  // 0 bad, 1 good, 2 not this kernel's page
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const uint64_t ntiles = (n + 15) / 16;
+    const uint64_t t = xcd_tile(blockIdx.x, ntiles);  // the launch covers every tile once
+    // results staged per tile: one coalesced store per tile instead of 16
+    // scattered 8-byte (1-byte) stores inside the read stream, +1.0-1.7 % on
+    // config 3 (profiles/r02/desc_staged_lab.txt); stamps write headers
+    constexpr bool staged = MODE != kStamp;
+    const int grp = threadIdx.x >> 4;
+    const uint64_t pg = t * 16 + grp;
+    uint8_t st = 2;
+    if (pg < n) {
+        const uint64_t o = off[pg];
+        const uint32_t P = len[pg];
+        if (xxh3_fast_ok(o, P)) {
+            const uint8_t* page = base + o;
+            uint64_t stored = 0;
+            const uint64_t h = B4 ? xxh3_page_rt4<NT>(page, P, L, stored) : xxh3_page_rt<NT>(page, P, L, stored);
+            if (!staged) {
+                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+            } else {
+                st = h == stored ? 1 : 0;
+                if (L.g == 0) tile_h[grp] = h;
+            }
+        } else if (xxh3_group_ok(P)) {  // off the chunk grid or unaligned: the any-size body
+            const uint8_t* page = base + o;
+            uint64_t stored = 0;
+            const uint64_t h = xxh3_page_any<NT>(page, P, L, stored);
+            if (!staged) {
+                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
+            } else {
+                st = h == stored ? 1 : 0;
+                if (L.g == 0) tile_h[grp] = h;
+            }
+        } else if (L.g == 0) {  // shorter than the long path: one lane, results written directly
+            if (P < 8) {  // shorter than its header: never valid (as generic_one)
+                if (MODE == kValidate) {
+                    ok[pg] = 0;
+                    if (out) out[pg] = 0;
+                    if (first_bad) note_bad(first_bad, pg);
+                } else if (MODE == kDigest) {
+                    out[pg] = 0;
+                }
+            } else {
+                const uint8_t* page = base + o;
+                const uint64_t h = xxh3_short(page + 8, P - 8);
+                if (MODE != kStamp) emit(MODE, pg, h, ld64(page), nullptr, out, ok, first_bad);
+            }
+        }
+    }
+    if (staged) {
+        if (L.g == 0) tile_st[grp] = st;
+        __syncthreads();
+        const uint64_t i = t * 16 + threadIdx.x;
+        const int s = threadIdx.x < 16 && i < n ? tile_st[threadIdx.x] : 2;
+        if (s != 2) {
+            if (MODE == kDigest || out) st_nt(out + i, tile_h[threadIdx.x]);
+            if (MODE == kValidate) st_nt(ok + i, (uint8_t)s);
+        }
+        if (MODE == kValidate && first_bad && threadIdx.x == 0) {
+            for (int k = 0; k < 16 && t * 16 + k < n; ++k)
+                if (tile_st[k] == 0) {
+                    note_bad(first_bad, t * 16 + k);
+                    break;
+                }
+        }
+    }
+}
+
 // One lane per range.  SKIP = 8 applies the page convention (hash [8, len),
-// stored digest in [0, 8)); SKIP = 0 hashes the raw range.  FILTER 1 (page
-// convention, seed 0, after the descriptor fast kernels): pages those kernels
-// took are skipped, and for XXH3 the other long-path pages (P >= 249: off the
-// 256-byte grid or unaligned) are hashed a 16-lane group per page with the
-// any-size body -- each wave ballots its lanes' such pages and works through
-// them four at a time.  FILTER 2: raw ranges k_xxh3_long took are skipped.
+// stored digest in [0, 8)); SKIP = 0 hashes the raw range.  FILTER 1: XXH64
+// pages k_xxh64_lds took are skipped; FILTER 2: raw XXH3 ranges k_xxh3_long
+// took are skipped.  (XXH3 descriptor pages never come here: k_xxh3_desc
+// takes every shape.)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ len, uint64_t n, int algo,
                                                      uint64_t seed, int skip, int filter, uint64_t* __restrict__ out,
                                                      uint8_t* __restrict__ ok, unsigned long long* first_bad) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const bool groups = filter == 1 && algo == 0;
-    const int lane = threadIdx.x & 63;
-    // wave-uniform trip count, so the ballot below sees the whole wave
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
-        const uint64_t i = i0 + lane;
-        bool grp = false;
-        if (i < n) {
-            const uint64_t o = off[i];
-            const uint32_t P = len[i];
-            if (filter == 2 && xxh3_long_ok(base + o, P)) {
-            } else if (filter == 1 && algo == 0 && xxh3_fast_ok(o, P)) {
-            } else if (filter == 1 && algo == 0 && xxh3_group_ok(P)) {
-                grp = true;
-            } else if (filter == 1 && algo == 1 && xxh64_lines_ok(o, P)) {
-            } else {
-                generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
-            }
-        }
-        if (!groups) continue;
-        uint64_t mask = __ballot(grp);
-        if (!mask) continue;
-        const Xxh3Lane L = make_xxh3_lane(lane & 15);
-        while (mask) {  // wave-uniform
-            uint64_t m = mask;
-            for (int k = 0; k < (lane >> 4); ++k) m &= m - 1;  // this group's page: the (lane / 16)-th set bit
-            if (m) {
-                const uint64_t pg = i0 + (uint64_t)(__builtin_ctzll(m));
-                const uint8_t* page = base + off[pg];
-                uint64_t stored = 0;
-                const uint64_t h = xxh3_page_any<true>(page, len[pg], L, stored);
-                if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
-            }
-            for (int k = 0; k < 4; ++k) mask &= mask - 1;
-        }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (filter == 1 && algo == 1 && xxh64_lines_ok(off[i], len[i])) continue;
+        if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
+        generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
     }
 }
 
@@ -1620,6 +1619,10 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
                 else L(false, false);
             }
 #undef L
+            // every page is the descriptor kernel's (fast body, any-size body,
+            // short pages on one lane): no generic pass, which cost 4.7-5.2 us
+            // per call on config 3 (profiles/r02d_sweep.json, r02e_sweep.json)
+            return hipGetLastError();
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
             if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
