@@ -197,6 +197,49 @@ def test_desc_odd_shapes(algo):
     assert np.array_equal(ok.cpu().numpy().astype(bool), lens >= 8)
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+def test_desc_random_shapes(algo, seed):
+    """Descriptor batches of random page sizes (0-20000 bytes, plus every
+    length-class and block edge) at random offsets of any alignment, in random
+    order: every branch of k_xxh3_desc (chunked body, any-size body, short
+    pages on one lane) and of the XXH64 path (LDS kernel, generic lanes) next
+    to each other in the same tiles.  Digest, stamp and validate vs the oracle."""
+    rng = np.random.default_rng(seed)
+    edges = np.array([0, 1, 7, 8, 9, 16, 24, 25, 136, 137, 248, 249, 250, 256, 257, 263, 264, 1032, 1033, 1040,
+                      1096, 2056, 4096, 4104, 8192, 8200, 16384, 65535], dtype=np.uint32)
+    n = 2500
+    lens = np.where(rng.random(n) < 0.25, edges[rng.integers(0, len(edges), n)],
+                    rng.integers(0, 20001, n)).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 40))
+        if rng.random() < 0.5:
+            pos = (pos + 15) // 16 * 16
+        offs[i] = pos
+        pos += int(lens[i])
+    perm = rng.permutation(n)  # descriptors not in memory order
+    offs, lens = offs[perm], lens[perm]
+    host = rng.integers(0, 256, size=pos + 64, dtype=np.uint8)
+    want = np.zeros(n, dtype=np.uint64)  # header-less pages (< 8 bytes) digest to 0 (the reference assumes >= 8)
+    hdr = lens >= 8
+    want[hdr] = oracle.desc_digest(host, offs[hdr], lens[hdr], algo)
+    base = torch.from_numpy(host).to(DEV)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+    got = u64(pcs.desc_digest(base, d_off, d_len, n, algo))
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, [(int(i), int(lens[i]), int(offs[i]) % 16) for i in bad[:8]]
+    pcs.desc_stamp(base, d_off, d_len, n, algo)
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
+    assert np.array_equal(ok.cpu().numpy().astype(bool), lens >= 8)
+    h2 = base.cpu().numpy()
+    for i in np.flatnonzero(lens >= 8)[:400]:
+        o = int(offs[i])
+        assert h2[o:o + 8].tobytes() == int(want[i]).to_bytes(8, "little")
+
+
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_desc_mixed_wide(algo):
     """Many pages of many sizes in random order: every kernel split of the
