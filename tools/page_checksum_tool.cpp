@@ -141,9 +141,10 @@ bool pwrite_full(int fd, const char* buf, uint64_t len, uint64_t off) {
 // pread of one chunk split over a few threads: a single thread's copy out of
 // the page cache (~6 GiB/s) would otherwise bound the scrub.
 // PCS_SCAN_THREADS / PCS_SCAN_PIECE_MIB / PCS_SCAN_CHUNK_MIB override the
-// reader threads (8), the read piece (8 MiB) and the chunk per batch (64 MiB);
-// tools/lab/scan_lab.sh sweeps them (more threads or larger chunks measured no
-// faster, profiles/r02/scan_lab.txt).
+// reader threads (16, at most the host's), the read piece (4 MiB) and the
+// chunk per batch (64 MiB); tools/lab/scan_lab.sh sweeps them: 16 x 4 MiB
+// against 8 x 8 MiB: 19.2-19.8 vs 13.5-14.9 GiB/s on a 1 GiB file, 25-31 vs
+// 27.5 on 4 GiB; 128 MiB chunks slower (profiles/r02/scan_lab.txt).
 uint64_t env_u64(const char* name, uint64_t dflt) {
     const char* v = std::getenv(name);
     uint64_t x;
@@ -151,8 +152,9 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 }
 
 bool pread_parallel(int fd, char* buf, uint64_t len, uint64_t off) {
-    static const uint64_t kThreads = env_u64("PCS_SCAN_THREADS", 8);
-    static const uint64_t kPiece = env_u64("PCS_SCAN_PIECE_MIB", 8) << 20;
+    static const uint64_t kThreads =
+        env_u64("PCS_SCAN_THREADS", std::min<uint64_t>(16, std::max(1u, std::thread::hardware_concurrency())));
+    static const uint64_t kPiece = env_u64("PCS_SCAN_PIECE_MIB", 4) << 20;
     const unsigned T = (unsigned)std::min<uint64_t>(kThreads, (len + kPiece - 1) / kPiece);
     if (T <= 1) return pread_full(fd, buf, len, off);
     std::vector<std::thread> th;
@@ -210,6 +212,16 @@ int bulk(bool stamp, const char* path, const char* size_s) {
         if (fb != UINT64_MAX) first_bad = std::min(first_bad, first[k] + fb);
         return true;
     };
+    {
+        // warm the GPU path (code-object load, first launch) before the clock
+        // starts: ~30 ms that would otherwise land on the first chunk of a
+        // scrub (a long-running service pays it once)
+        std::memset(buf[0], 0, (size_t)P);
+        const void* one = buf[0];
+        if (pcs_batch_submit(batch[0], stamp ? PCS_BATCH_DIGEST : PCS_BATCH_VALIDATE, &one, P, 1, PCS_XXH3_64,
+                             PCS_FLAG_NONE) == PCS_OK)
+            (void)pcs_batch_wait(batch[0]);
+    }
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t k = 0;
     for (uint64_t p0 = 0; p0 < n; p0 += chunk, ++k) {
