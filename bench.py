@@ -291,6 +291,31 @@ CONFIG1_SEED = 0x5EED0001
 CONFIG1_PAGES = 1 << 18  # 1 GiB of 4 KiB pages (BASELINE configs[0])
 
 
+CONFIG1_DIR = os.path.join(ROOT, ".bench_tmp")  # git- and gpurun-ignored; not gpurun_out/ (1 GiB)
+
+
+def config1_workdir(need_bytes: int, workdir: str | None = None) -> str:
+    """A directory with room for the config-1 file: the working tree first
+    (the GPU box's scratch copy), then the system temp dir.  Raises with the
+    free space of each candidate if none has `need_bytes` plus 256 MiB."""
+    import shutil
+    import tempfile
+
+    cands = [workdir] if workdir else [CONFIG1_DIR, tempfile.gettempdir()]
+    seen = []
+    for c in cands:
+        try:
+            os.makedirs(c, exist_ok=True)
+            free = shutil.disk_usage(c).free
+        except OSError as e:
+            seen.append(f"{c}: {e}")
+            continue
+        if free >= need_bytes + (256 << 20):
+            return c
+        seen.append(f"{c}: {free >> 20} MiB free")
+    raise RuntimeError(f"no room for the {need_bytes >> 20} MiB config-1 file ({'; '.join(seen)})")
+
+
 def config1(target_s: float, all_cores_s: float | None, workdir: str | None = None):
     """BASELINE config 1: the reference checksum over a 1 GiB file of 4 KiB
     pages on ONE host thread (tools/page_checksum_tool.cpp reads a page from
@@ -311,8 +336,10 @@ def config1(target_s: float, all_cores_s: float | None, workdir: str | None = No
 
     import oracle  # baseline infrastructure only
 
+    if os.environ.get("PCS_BENCH_FAIL_CONFIG1"):  # tests: a failing leg must not lose the line
+        raise RuntimeError("PCS_BENCH_FAIL_CONFIG1 set")
     P, n = 4096, CONFIG1_PAGES
-    d = tempfile.mkdtemp(prefix="pcs_config1_", dir=workdir)
+    d = tempfile.mkdtemp(prefix="pcs_config1_", dir=config1_workdir(n * P, workdir))
     path = os.path.join(d, "config1.data")
     try:
         r = subprocess.run([pcs.TOOL_PATH, "--gen", path, str(n), str(P), hex(CONFIG1_SEED)],
@@ -458,7 +485,7 @@ def batch_latency(pool, pageable, w: Workload):
             ts = []
             for _ in range(200):
                 t0 = time.perf_counter()
-                fn(ptrs.ctypes.data, w.P, nb, w.algo, ok.ctypes.data, ctypes.byref(fb), 0)
+                fn(ptrs.ctypes.data, w.P, nb, w.algo, ok.ctypes.data, ctypes.byref(fb))
                 ts.append(time.perf_counter() - t0)
             row[name] = round(float(np.median(ts[20:])) * 1e6, 1)
         b = pcs.Batch()
@@ -505,47 +532,63 @@ SWEEP = (
 PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits the kernel trace on it
 
 
-def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale: int = 1):
+def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale: int = 1,
+          deadline: float | None = None):
     """Each entry on a device-resident workload that stays allocated until the
     sweep ends: config 2 entries reuse the headline's batch (`head`), config 3
     XXH64 reuses config 3's arena.  Nothing is freed between entries: a
     hipFree of a large buffer (torch.cuda.empty_cache) left every other buffer
     of the process reading ~1.5 % slower until another process initialised
-    the GPU (tools/lab/degrade_lab.py, profiles/r02/degrade_lab.txt)."""
+    the GPU (tools/lab/degrade_lab.py, profiles/r02/degrade_lab.txt).
+
+    An entry that raises is recorded as {"key", "error"} and the sweep goes
+    on; entries that would start after `deadline` (perf_counter seconds) are
+    recorded as {"key", "skipped"} so the bench stays inside its wall budget."""
     out = []
     resident: dict[int, Workload] = {}
     if head is not None and head.cfg == 2 and head.n == CONFIGS[2][1] // scale:
         resident[2] = head
     for key, cfg, algo, mode in SWEEP:
-        if cfg not in resident:
-            resident[cfg] = Workload(cfg, algo, 0, max(1, CONFIGS[cfg][1] // scale), dev)
-        w = resident[cfg]
-        w.algo = algo
-        if mode == "validate":
-            w.step("stamp")
-        torch.cuda.synchronize()
-        time.sleep(PHASE_GAP_S)
-        t_wall0 = time.perf_counter()
-        avg = timed_launches(w, mode, steps, warmup)
-        t_wall = time.perf_counter() - t_wall0
-        time.sleep(PHASE_GAP_S)
-        alg = w.algorithmic_bytes(mode)
-        if mode != "stamp":
-            w.step("digest")  # w.out = this batch's digests for the parity sample
-            torch.cuda.synchronize()
-        par = parity_sample(w, mode)
-        drill = w.corruption_drill()
-        traffic = committed_traffic_key(key)
-        e = {"key": key, "config": cfg, "workload": w.desc, "algo": "xxh3_64" if algo == 0 else "xxh64",
-             "mode": mode, "pages": w.n, "bytes": w.bytes, "steps": steps, "warmup": warmup,
-             "avg_launch_ms": round(avg * 1e3, 4), "GiBps": round(w.bytes / avg / GIB, 1),
-             "achieved_GBps": round(alg / avg / 1e9, 1), "frac": round(alg / avg / 1e9 / HBM_PEAK_GBPS, 4),
-             "algorithmic_bytes_per_launch": alg, "wall_s": round(t_wall, 3),
-             "traffic": traffic[0] if traffic else None, "traffic_source": traffic[1] if traffic else None,
-             "parity": par, "corruption_drill": drill}
-        out.append(e)
+        if deadline is not None and time.perf_counter() > deadline:
+            out.append({"key": key, "config": cfg, "skipped": "bench wall budget spent"})
+            continue
+        try:
+            out.append(sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale))
+        except Exception as e:  # noqa: BLE001 — recorded in the line, never loses it
+            out.append({"key": key, "config": cfg, "error": f"{type(e).__name__}: {e}"[:500]})
         time.sleep(PHASE_GAP_S)
     return out
+
+
+def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale):
+    """One sweep entry (see sweep())."""
+    if cfg not in resident:
+        resident[cfg] = Workload(cfg, algo, 0, max(1, CONFIGS[cfg][1] // scale), dev)
+    w = resident[cfg]
+    w.algo = algo
+    if mode == "validate":
+        w.step("stamp")
+    torch.cuda.synchronize()
+    time.sleep(PHASE_GAP_S)
+    t_wall0 = time.perf_counter()
+    avg = timed_launches(w, mode, steps, warmup)
+    t_wall = time.perf_counter() - t_wall0
+    time.sleep(PHASE_GAP_S)
+    alg = w.algorithmic_bytes(mode)
+    if mode != "stamp":
+        w.step("digest")  # w.out = this batch's digests for the parity sample
+        torch.cuda.synchronize()
+    par = parity_sample(w, mode)
+    drill = w.corruption_drill()
+    traffic = committed_traffic_key(key)
+    e = {"key": key, "config": cfg, "workload": w.desc, "algo": "xxh3_64" if algo == 0 else "xxh64",
+         "mode": mode, "pages": w.n, "bytes": w.bytes, "steps": steps, "warmup": warmup,
+         "avg_launch_ms": round(avg * 1e3, 4), "GiBps": round(w.bytes / avg / GIB, 1),
+         "achieved_GBps": round(alg / avg / 1e9, 1), "frac": round(alg / avg / 1e9 / HBM_PEAK_GBPS, 4),
+         "algorithmic_bytes_per_launch": alg, "wall_s": round(t_wall, 3),
+         "traffic": traffic[0] if traffic else None, "traffic_source": traffic[1] if traffic else None,
+         "parity": par, "corruption_drill": drill}
+    return e
 
 
 def committed_traffic_key(key: str):
@@ -580,6 +623,18 @@ def committed_traffic(cfg: int, algo: int):
     return best
 
 
+def guarded(name: str, fn, *a, **kw):
+    """fn(*a, **kw), or {"error": ...} if it raises (the traceback goes to
+    stderr): an optional leg never takes the headline line down with it."""
+    try:
+        r = fn(*a, **kw)
+        return r if r is not None else {"error": f"{name}: no result (reference build absent)"}
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        return {"error": f"{name}: {type(e).__name__}: {e}"[:500]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -601,18 +656,24 @@ def main():
                     help="divide every sweep workload's page count (tests only; default 1 = the BASELINE sizes)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the host-memory path (pinned direct DMA and pageable gather)")
+    ap.add_argument("--wall-budget", type=float, default=360.0,
+                    help="seconds from start after which the optional legs (config 1, host-inclusive, "
+                         "sweep entries) are skipped and recorded as such; the headline line always prints")
     args = ap.parse_args()
+    t_start = time.perf_counter()
+    deadline = t_start + args.wall_budget
 
     world, rank, local = dist_env()
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     if args.config == 1:  # BASELINE configs[0]: CPU reference only, runs without a GPU
         if rank == 0:
-            c1 = config1(args.cpu_seconds, None if args.no_all_cores else min(args.cpu_seconds, 5.0))
-            one = c1["cpu_baseline"]
+            c1 = guarded("config1", config1, args.cpu_seconds,
+                         None if args.no_all_cores else min(args.cpu_seconds, 5.0))
+            one = c1.get("cpu_baseline") or {}
             print(json.dumps({"metric": "GiB/s page_checksum_tool-style validate over a 1 GiB file of 4 KiB pages, "
                                         "reference xxHash on one host thread",
-                              "value": one["value"], "unit": "GiB/s", "n_gpus": 0, "higher_is_better": True,
+                              "value": one.get("value"), "unit": "GiB/s", "n_gpus": 0, "higher_is_better": True,
                               "dtype": "u64", "data": "synthetic (splitmix64 pages, seed 0x5EED0001)",
                               "config": {"workload": "config1: 1 GiB file, 4 KiB pages, single host thread"},
                               **c1}), flush=True)
@@ -694,14 +755,26 @@ def main():
     time.sleep(PHASE_GAP_S)
     drill = w.corruption_drill() if rank == 0 else None
     time.sleep(PHASE_GAP_S)
-    hostinc = host_inclusive(w) if args.host_inclusive and rank == 0 else None
-    sweep_entries = None
-    if rank == 0 and world == 1 and not args.no_sweep:
-        sweep_entries = sweep(dev, args.sweep_steps, args.sweep_warmup, head=w if algo == 0 else None,
-                              scale=max(1, args.sweep_scale))
+    # Optional legs, each guarded: a failure is recorded under its key and the
+    # headline line (roofline, parity, drill) still prints.  Config 1 runs first
+    # since cpu_baseline belongs to the contract line; the sweep is last and
+    # skips entries past the wall budget.
     c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        c1 = config1(args.cpu_seconds, None if args.no_all_cores else min(args.cpu_seconds, 5.0))
+        all_s = None if args.no_all_cores else min(args.cpu_seconds, 5.0)
+        need = args.cpu_seconds + (all_s or 0) + 3.0 + 30.0  # + port leg + gen/scan/warm margin
+        if time.perf_counter() + need > deadline:
+            c1 = {"skipped": f"bench wall budget: {deadline - time.perf_counter():.0f} s left, ~{need:.0f} s needed"}
+        else:
+            c1 = guarded("config1", config1, args.cpu_seconds, all_s)
+    hostinc = None
+    if args.host_inclusive and rank == 0:
+        hostinc = guarded("host_inclusive", host_inclusive, w) if time.perf_counter() < deadline else \
+            {"skipped": "bench wall budget spent"}
+    sweep_entries = None
+    if rank == 0 and world == 1 and not args.no_sweep:
+        sweep_entries = guarded("sweep", sweep, dev, args.sweep_steps, args.sweep_warmup,
+                                head=w if algo == 0 else None, scale=max(1, args.sweep_scale), deadline=deadline)
 
     if rank == 0:
         achieved = w.algorithmic_bytes(args.mode) / avg_launch / 1e9
@@ -746,14 +819,17 @@ def main():
                 "launch_timing": f"HIP events bracketing the {args.steps} timed steps on the launch stream",
             },
             "stream_read_GBps": round(stream_rate, 1) if stream_rate else None,
-            "cpu_baseline": c1["cpu_baseline"] if c1 else None,
+            "cpu_baseline": c1.get("cpu_baseline") if c1 else None,
             "parity": parity,
         }
         line["corruption_drill"] = drill
         if c1 is not None:
-            line["cpu_all_cores"] = c1["cpu_all_cores"]
-            line["cpu_port"] = c1["cpu_port"]
-            line["cli_scan"] = c1["cli_scan"]
+            for k in ("cpu_all_cores", "cpu_port", "cli_scan"):
+                line[k] = c1.get(k)
+            for k in ("error", "skipped"):
+                if k in c1:
+                    line[f"config1_{k}"] = c1[k]
+        line["bench_wall_s"] = round(time.perf_counter() - t_start, 1)
         if scaling is not None:
             line["scaling_detail"] = scaling
         if hostinc is not None:

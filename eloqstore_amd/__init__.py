@@ -51,7 +51,8 @@ _SIGS = {
     "pcs_desc_stamp_dev": [_vp, _vp, _vp, _u64, _i32, _vp],
     "pcs_xxh3_64_ranges_dev": [_vp, _vp, _vp, _u64, _vp, _vp],
     "pcs_xxh64_ranges_dev": [_vp, _vp, _vp, _u64, _u64, _vp, _vp],
-    "pcs_pages_validate_host": [_vp, _u64, _u64, _i32, _vp, _vp, _u32],
+    "pcs_pages_validate_host": [_vp, _u64, _u64, _i32, _vp, _vp],
+    "pcs_pages_validate_host_ex": [_vp, _u64, _u64, _i32, _vp, _vp, _u32],
     "pcs_pages_stamp_host": [_vp, _u64, _u64, _i32],
     "pcs_pages_digest_host": [_vp, _u64, _u64, _i32, _vp],
     "pcs_shard_range": [_u64, _i32, _i32, _P(_u64), _P(_u64)],
@@ -64,7 +65,8 @@ _SIGS = {
     "pcs_host_register": [_vp, _u64],
     "pcs_host_unregister": [_vp],
     "pcs_batch_create": [_P(_vp)],
-    "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32, _u32],
+    "pcs_batch_submit": [_vp, _i32, _vp, _u64, _u64, _i32],
+    "pcs_batch_submit_ex": [_vp, _i32, _vp, _u64, _u64, _i32, _u32],
     "pcs_batch_poll": [_vp],
     "pcs_batch_wait": [_vp],
     "pcs_batch_result": [_vp, _vp, _vp, _vp],
@@ -291,7 +293,7 @@ class Batch:
         self._keep = (arr, keep)
         self.n = len(pages)
         self.mode = mode
-        _call("pcs_batch_submit", self._b, mode, arr, page_size, len(pages), algo, _flags(skip_verify))
+        _call("pcs_batch_submit_ex", self._b, mode, arr, page_size, len(pages), algo, _flags(skip_verify))
 
     def submit_ptrs(self, mode: int, ptrs, page_size: int, algo: int = XXH3_64, skip_verify: bool = False) -> None:
         """Submit raw page addresses (a uint64 array of host pointers)."""
@@ -299,7 +301,8 @@ class Batch:
         self._keep = ptrs
         self.n = len(ptrs)
         self.mode = mode
-        _call("pcs_batch_submit", self._b, mode, ptrs.ctypes.data, page_size, len(ptrs), algo, _flags(skip_verify))
+        _call("pcs_batch_submit_ex", self._b, mode, ptrs.ctypes.data, page_size, len(ptrs), algo,
+              _flags(skip_verify))
 
     def poll(self) -> bool:
         rc = lib().pcs_batch_poll(self._b)
@@ -359,7 +362,7 @@ def validate_checksum(page) -> bool:
     buf = page if isinstance(page, bytearray) else bytearray(page)
     arr, _keep = _page_ptrs([buf])
     ok = (ctypes.c_uint8 * 1)()
-    _call("pcs_pages_validate_host", arr, len(buf), 1, XXH3_64, ok, None, FLAG_NONE)
+    _call("pcs_pages_validate_host", arr, len(buf), 1, XXH3_64, ok, None)
     return bool(ok[0])
 
 
@@ -368,7 +371,8 @@ def validate_checksums(pages: list, page_size: int, algo: int = XXH3_64, skip_ve
     arr, _keep = _page_ptrs(pages)
     ok = (ctypes.c_uint8 * max(1, len(pages)))()
     fb = ctypes.c_uint64(0)
-    _call("pcs_pages_validate_host", arr, page_size, len(pages), algo, ok, ctypes.byref(fb), _flags(skip_verify))
+    _call("pcs_pages_validate_host_ex", arr, page_size, len(pages), algo, ok, ctypes.byref(fb),
+          _flags(skip_verify))
     return list(ok), (None if fb.value == (1 << 64) - 1 else fb.value)
 
 
@@ -396,12 +400,12 @@ def host_unregister(addr: int) -> None:
 
 
 def validate_ptrs(ptrs, page_size: int, algo: int = XXH3_64, skip_verify: bool = False):
-    """pcs_pages_validate_host over raw host page addresses -> (ok array, first_bad or None)."""
+    """pcs_pages_validate_host_ex over raw host page addresses -> (ok array, first_bad or None)."""
     ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
     ok = np.zeros(max(1, len(ptrs)), dtype=np.uint8)
     fb = ctypes.c_uint64(0)
-    _call("pcs_pages_validate_host", ptrs.ctypes.data, page_size, len(ptrs), algo, ok.ctypes.data, ctypes.byref(fb),
-          _flags(skip_verify))
+    _call("pcs_pages_validate_host_ex", ptrs.ctypes.data, page_size, len(ptrs), algo, ok.ctypes.data,
+          ctypes.byref(fb), _flags(skip_verify))
     return ok[: len(ptrs)], (None if fb.value == (1 << 64) - 1 else fb.value)
 
 

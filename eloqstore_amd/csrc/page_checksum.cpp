@@ -32,7 +32,7 @@ bool ValidateChecksum(std::string_view blob) {
     if (blob.size() < kChecksumBytes) return false;
     const void* page = blob.data();
     uint8_t ok = 0;
-    if (int rc = pcs_pages_validate_host(&page, blob.size(), 1, PCS_XXH3_64, &ok, nullptr, PCS_FLAG_NONE))
+    if (int rc = pcs_pages_validate_host(&page, blob.size(), 1, PCS_XXH3_64, &ok, nullptr))
         die("ValidateChecksum", rc);
     return ok != 0;
 }
@@ -41,9 +41,9 @@ size_t ValidateChecksums(std::span<const char* const> pages, size_t page_size, u
                          bool skip_verify) {
     uint64_t first_bad = UINT64_MAX;
     static_assert(sizeof(const char*) == sizeof(const void*));
-    if (int rc = pcs_pages_validate_host(reinterpret_cast<const void* const*>(pages.data()), page_size, pages.size(),
-                                         static_cast<int>(hash), ok_out, &first_bad,
-                                         skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
+    if (int rc = pcs_pages_validate_host_ex(reinterpret_cast<const void* const*>(pages.data()), page_size,
+                                            pages.size(), static_cast<int>(hash), ok_out, &first_bad,
+                                            skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
         die("ValidateChecksums", rc);
     return first_bad == UINT64_MAX ? pages.size() : static_cast<size_t>(first_bad);
 }
@@ -80,9 +80,9 @@ void ChecksumBatch::SubmitValidate(std::span<const char* const> pages, size_t pa
     validate_ = true;
     collected_ = false;
     ok_.assign(n_, 0);
-    if (int rc = pcs_batch_submit(batch_, PCS_BATCH_VALIDATE, reinterpret_cast<const void* const*>(pages.data()),
-                                  page_size, n_, static_cast<int>(hash),
-                                  skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
+    if (int rc = pcs_batch_submit_ex(batch_, PCS_BATCH_VALIDATE, reinterpret_cast<const void* const*>(pages.data()),
+                                     page_size, n_, static_cast<int>(hash),
+                                     skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
         die("ChecksumBatch::SubmitValidate", rc);
 }
 
@@ -91,7 +91,7 @@ void ChecksumBatch::SubmitStamp(std::span<char* const> pages, size_t page_size, 
     validate_ = false;
     collected_ = false;
     if (int rc = pcs_batch_submit(batch_, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(pages.data()),
-                                  page_size, n_, static_cast<int>(hash), PCS_FLAG_NONE))
+                                  page_size, n_, static_cast<int>(hash)))
         die("ChecksumBatch::SubmitStamp", rc);
 }
 

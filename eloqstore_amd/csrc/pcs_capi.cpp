@@ -488,6 +488,7 @@ struct pcs_batch {
     bool zero_copy = false;  // in-flight batch reads registered pages in place
     uint64_t n = 0, P = 0, first_bad = UINT64_MAX;
     int mode = 0, state = 0;  // 0 idle, 1 in flight, 2 done, -1 failed
+    bool all_ok = false;      // completed at submit with nothing hashed (skip_verify / empty)
 };
 
 namespace {
@@ -519,7 +520,7 @@ int batch_finalize(pcs_batch* b) {
 
 extern "C" {
 
-const char* pcs_version(void) { return "eloqstore-pcs 0.1.0 (gfx950; xxHash v0.8.3 page path)"; }
+const char* pcs_version(void) { return "eloqstore-pcs 0.3.0 (gfx950; xxHash v0.8.3 page path)"; }
 
 const char* pcs_last_error(void) { return t_last_error.c_str(); }
 
@@ -581,7 +582,12 @@ int pcs_xxh64_ranges_dev(const void* d_base, const uint64_t* d_off, const uint32
 }
 
 int pcs_pages_validate_host(const void* const* pages, uint64_t page_size, uint64_t n_pages, int algo, uint8_t* ok,
-                            uint64_t* first_bad, uint32_t flags) {
+                            uint64_t* first_bad) {
+    return pcs_pages_validate_host_ex(pages, page_size, n_pages, algo, ok, first_bad, PCS_FLAG_NONE);
+}
+
+int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uint64_t n_pages, int algo, uint8_t* ok,
+                               uint64_t* first_bad, uint32_t flags) {
     if (n_pages && !ok) return fail(PCS_ERR_INVALID, "ok is null");
     if (int rc = check_flags(flags)) return rc;
     if (flags & PCS_FLAG_SKIP_VERIFY) {  // kv_options.h:41: the validate loop is not run
@@ -665,8 +671,12 @@ int pcs_batch_create(pcs_batch** out) {
     return PCS_OK;
 }
 
-int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo,
-                     uint32_t flags) {
+int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo) {
+    return pcs_batch_submit_ex(b, mode, pages, P, n, algo, PCS_FLAG_NONE);
+}
+
+int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo,
+                        uint32_t flags) {
     if (!b) return fail(PCS_ERR_INVALID, "batch is null");
     if (b->state == 1) return fail(PCS_ERR_INVALID, "batch already in flight");
     // From here on the previous batch's results are gone: a submit that fails
@@ -675,11 +685,24 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
     b->state = 0;
     b->n = 0;
     b->first_bad = UINT64_MAX;
+    b->all_ok = false;
     if (mode < 0 || mode > 2) return fail(PCS_ERR_INVALID, "bad batch mode");
     if (int rc = check_flags(flags)) return rc;
     if ((flags & PCS_FLAG_SKIP_VERIFY) && mode != PCS_BATCH_VALIDATE)
         return fail(PCS_ERR_INVALID, "PCS_FLAG_SKIP_VERIFY applies to validate batches only");
     if (int rc = check_host_batch_args(pages, P, n, algo)) return rc;
+    if (n == 0 || (flags & PCS_FLAG_SKIP_VERIFY)) {
+        // nothing to hash: complete at submit, before any staging is sized
+        // (a skipped batch allocates and pins nothing; result() reports 1s)
+        b->mode = mode;
+        b->n = n;
+        b->P = P;
+        b->zero_copy = false;
+        b->stamp_pages.clear();
+        b->all_ok = true;
+        b->state = 2;
+        return PCS_OK;
+    }
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
     hipError_t e = hipSuccess;
@@ -715,12 +738,6 @@ int pcs_batch_submit(pcs_batch* b, int mode, const void* const* pages, uint64_t 
     b->stamp_pages.assign(n, nullptr);
     if (mode == PCS_BATCH_STAMP)
         for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
-    if (n == 0 || (flags & PCS_FLAG_SKIP_VERIFY)) {  // nothing to hash: complete at submit
-        if (n) std::memset(b->h_ok, 1, n);
-        b->state = 2;
-        b->first_bad = UINT64_MAX;
-        return PCS_OK;
-    }
     hipStream_t s = b->stream;
     b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
     if (b->zero_copy) {
@@ -786,11 +803,14 @@ int pcs_batch_result(pcs_batch* b, uint8_t* ok, uint64_t* digests, uint64_t* fir
     if (b->state != 2) return fail(PCS_ERR_INVALID, "batch not complete");
     if (ok) {
         if (b->mode != PCS_BATCH_VALIDATE) return fail(PCS_ERR_INVALID, "verdicts exist only in validate mode");
-        std::memcpy(ok, b->h_ok, b->n);
+        if (b->all_ok)
+            std::memset(ok, 1, b->n);
+        else
+            std::memcpy(ok, b->h_ok, b->n);
     }
     if (digests) {
         if (b->mode == PCS_BATCH_VALIDATE) return fail(PCS_ERR_INVALID, "digests exist in digest/stamp mode");
-        std::memcpy(digests, b->h_dig, b->n * 8);
+        if (b->n) std::memcpy(digests, b->h_dig, b->n * 8);
     }
     if (first_bad) *first_bad = b->first_bad;
     return PCS_OK;

@@ -63,8 +63,10 @@ enum pcs_algo {
     PCS_XXH64 = 1,   /* XXH64, seed 0 */
 };
 
-/* Flags of the validating host entry points (pcs_pages_validate_host,
- * pcs_batch_submit in PCS_BATCH_VALIDATE mode).
+/* Flags of the validating host entry points (pcs_pages_validate_host_ex,
+ * pcs_batch_submit_ex in PCS_BATCH_VALIDATE mode).  The flag-less names keep
+ * their original 6-argument prototypes (= PCS_FLAG_NONE, always verify), so a
+ * caller built against an older header can never pass a stray flag word.
  *   PCS_FLAG_SKIP_VERIFY  KvOptions::skip_verify_checksum (include/kv_options.h:41):
  *                         the reference skips the validate loop entirely
  *                         (async_io_manager.cpp:239, 353); here nothing is
@@ -131,7 +133,10 @@ int pcs_xxh64_ranges_dev(const void *d_base, const uint64_t *d_off, const uint32
  * flow through three slots (H2D || kernel || D2H).  Safe to call concurrently
  * from several host threads (each thread owns its staging and streams). */
 int pcs_pages_validate_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
-                            int algo, uint8_t *ok, uint64_t *first_bad, uint32_t flags);
+                            int algo, uint8_t *ok, uint64_t *first_bad);
+/* The same plus a flags word: PCS_FLAG_SKIP_VERIFY = KvOptions::skip_verify_checksum. */
+int pcs_pages_validate_host_ex(const void *const *pages, uint64_t page_size, uint64_t n_pages,
+                               int algo, uint8_t *ok, uint64_t *first_bad, uint32_t flags);
 int pcs_pages_stamp_host(void *const *pages, uint64_t page_size, uint64_t n_pages, int algo);
 int pcs_pages_digest_host(const void *const *pages, uint64_t page_size, uint64_t n_pages,
                           int algo, uint64_t *digests);
@@ -172,11 +177,14 @@ int pcs_host_unregister(void *ptr);  /* ptr = the base passed to pcs_host_regist
 typedef struct pcs_batch pcs_batch;
 enum pcs_batch_mode { PCS_BATCH_DIGEST = 0, PCS_BATCH_VALIDATE = 1, PCS_BATCH_STAMP = 2 };
 int pcs_batch_create(pcs_batch **out);  /* on the calling thread's current device */
-/* flags: PCS_FLAG_SKIP_VERIFY (validate mode only) completes the batch at
- * submit with every verdict 1.  A submit that fails leaves the batch idle:
- * poll/wait/result then refuse until a later submit succeeds. */
+/* A submit that fails leaves the batch idle: poll/wait/result then refuse
+ * until a later submit succeeds. */
 int pcs_batch_submit(pcs_batch *b, int mode, const void *const *pages, uint64_t page_size,
-                     uint64_t n_pages, int algo, uint32_t flags);
+                     uint64_t n_pages, int algo);
+/* flags: PCS_FLAG_SKIP_VERIFY (validate mode only) completes the batch at
+ * submit with every verdict 1, sizing and pinning no staging. */
+int pcs_batch_submit_ex(pcs_batch *b, int mode, const void *const *pages, uint64_t page_size,
+                        uint64_t n_pages, int algo, uint32_t flags);
 int pcs_batch_poll(pcs_batch *b);   /* 1 = done, 0 = in flight, < 0 = error */
 int pcs_batch_wait(pcs_batch *b);   /* blocks until done; PCS_OK or error */
 /* After completion: verdicts / digests (either may be NULL) and the first

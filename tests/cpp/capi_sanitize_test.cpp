@@ -79,7 +79,8 @@ static void no_device() {
     void* wpages[1] = {page.data()};
     uint64_t dig = 0, fb = 0;
     CHECK(pcs_pages_digest_host(pages, 4096, 1, PCS_XXH3_64, &dig) == PCS_ERR_NO_DEVICE);
-    CHECK(pcs_pages_validate_host(pages, 4096, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_NONE) == PCS_ERR_NO_DEVICE);
+    CHECK(pcs_pages_validate_host(pages, 4096, 1, PCS_XXH3_64, ok, &fb) == PCS_ERR_NO_DEVICE);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_NONE) == PCS_ERR_NO_DEVICE);
     CHECK(pcs_pages_stamp_host(wpages, 4096, 1, PCS_XXH3_64) == PCS_ERR_NO_DEVICE);
     CHECK(page[0] == 0xAB);  // nothing written without a device
     CHECK(pcs_manifest_checksum_host(page.data(), 100, &dig) == PCS_ERR_NO_DEVICE);
@@ -101,22 +102,23 @@ static void arguments() {
     // skip_verify (kv_options.h:41): argument checks only, every page passes, no device needed
     uint64_t fb = 0;
     std::memset(ok, 0, sizeof ok);
-    CHECK(pcs_pages_validate_host(pages, 4096, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_OK);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_OK);
     CHECK(ok[0] == 1 && fb == UINT64_MAX);
-    CHECK(pcs_pages_validate_host(pages, 4096, 0, PCS_XXH3_64, nullptr, nullptr, PCS_FLAG_SKIP_VERIFY) == PCS_OK);
-    CHECK(pcs_pages_validate_host(pages, 4096, 2, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
-    CHECK(pcs_pages_validate_host(pages, 4, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
-    CHECK(pcs_pages_validate_host(pages, 4096, 1, 9, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
-    CHECK(pcs_pages_validate_host(pages, 4096, 1, PCS_XXH3_64, nullptr, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
-    CHECK(pcs_pages_validate_host(pages, 4096, 1, PCS_XXH3_64, ok, &fb, 0x80) == PCS_ERR_INVALID);
-    CHECK(pcs_pages_validate_host(nullptr, 4096, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 0, PCS_XXH3_64, nullptr, nullptr, PCS_FLAG_SKIP_VERIFY) == PCS_OK);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 2, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(pages, 4, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 1, 9, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 1, PCS_XXH3_64, nullptr, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 1, PCS_XXH3_64, ok, &fb, 0x80) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(nullptr, 4096, 1, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
     // n * page_size past 2^64 is refused before any page pointer is read
-    CHECK(pcs_pages_validate_host(pages, 4096, 1ull << 53, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
+    CHECK(pcs_pages_validate_host_ex(pages, 4096, 1ull << 53, PCS_XXH3_64, ok, &fb, PCS_FLAG_SKIP_VERIFY) == PCS_ERR_INVALID);
     CHECK(std::strstr(pcs_last_error(), "overflows") != nullptr);
     CHECK(pcs_pages_digest_host(pages, 4096, 1, PCS_XXH3_64, nullptr) == PCS_ERR_INVALID);
     // batches: null handles
     CHECK(pcs_batch_create(nullptr) == PCS_ERR_INVALID);
-    CHECK(pcs_batch_submit(nullptr, 0, pages, 4096, 1, 0, 0) == PCS_ERR_INVALID);
+    CHECK(pcs_batch_submit(nullptr, 0, pages, 4096, 1, 0) == PCS_ERR_INVALID);
+    CHECK(pcs_batch_submit_ex(nullptr, 0, pages, 4096, 1, 0, 0) == PCS_ERR_INVALID);
     CHECK(pcs_batch_poll(nullptr) == PCS_ERR_INVALID);
     CHECK(pcs_batch_wait(nullptr) == PCS_ERR_INVALID);
     CHECK(pcs_batch_result(nullptr, ok, dummy, &fb) == PCS_ERR_INVALID);

@@ -133,7 +133,9 @@ static void test_concurrent() {
             std::vector<const void*> pages(16);
             std::vector<uint64_t> dev(pages.size());
             uint64_t x = 0x9E3779B97F4A7C15ull * (t + 1);
-            while (!stop.load(std::memory_order_relaxed)) {
+            // at least 2000 batches per reader even if the writers finish
+            // before this thread is scheduled (a loaded sanitizer run)
+            for (int iter = 0; iter < 2000 || !stop.load(std::memory_order_relaxed); ++iter) {
                 // a batch from one pool chunk (the common case) or, every 4th, from two
                 x ^= x << 13, x ^= x >> 7, x ^= x << 17;
                 const int s0 = (int)(x % kSlots), s1 = (x & 3) ? s0 : (int)((x >> 20) % kSlots);

@@ -1,0 +1,49 @@
+"""bench.py cannot lose its line (VERDICT r02 Next #1): every optional leg
+(config 1, host-inclusive, sweep entries) is guarded and wall-budgeted.  CPU
+checks of the guards themselves; the GPU halves are in test_gpu_bench.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+import bench  # noqa: E402
+
+
+def test_guarded_records_error_and_passes_results():
+    def boom():
+        raise RuntimeError("disk full")
+
+    r = bench.guarded("config1", boom)
+    assert r == {"error": "config1: RuntimeError: disk full"}
+    assert bench.guarded("x", lambda a, b=0: {"v": a + b}, 1, b=2) == {"v": 3}
+    assert "error" in bench.guarded("config1", lambda: None)
+
+
+def test_sweep_past_deadline_skips_every_entry_without_touching_the_gpu():
+    out = bench.sweep("cuda:0", 3, 1, deadline=0.0)
+    assert [e["key"] for e in out] == [s[0] for s in bench.SWEEP]
+    assert all("skipped" in e for e in out)
+
+
+def test_config1_workdir_prefers_the_tree_and_reports_space(tmp_path):
+    assert bench.config1_workdir(1 << 20, str(tmp_path)) == str(tmp_path)
+    with pytest.raises(RuntimeError, match="no room"):
+        bench.config1_workdir(1 << 62, str(tmp_path))
+
+
+def test_config1_failure_still_prints_the_line():
+    """--config 1 with the leg forced to raise: exit 0, one JSON line carrying
+    the error (the default N=1 run prints its headline the same way:
+    test_gpu_bench.py::test_bench_line_survives_failing_config1)."""
+    env = dict(os.environ, PCS_BENCH_FAIL_CONFIG1="1")
+    r = subprocess.run([sys.executable, "bench.py", "--config", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert "PCS_BENCH_FAIL_CONFIG1" in d["error"] and d["value"] is None

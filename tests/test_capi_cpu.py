@@ -136,9 +136,9 @@ def test_skip_verify_flag_needs_no_gpu():
     arr, _keep = pcs._page_ptrs(pages)
     okb = (ctypes.c_uint8 * 5)()
     fbv = ctypes.c_uint64()
-    assert so.pcs_pages_validate_host(arr, 4096, 5, 7, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
-    assert so.pcs_pages_validate_host(arr, 4, 5, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
-    assert so.pcs_pages_validate_host(arr, 4096, 5, 0, okb, ctypes.byref(fbv), 2) == pcs.PCS_ERR_INVALID
+    assert so.pcs_pages_validate_host_ex(arr, 4096, 5, 7, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
+    assert so.pcs_pages_validate_host_ex(arr, 4, 5, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
+    assert so.pcs_pages_validate_host_ex(arr, 4096, 5, 0, okb, ctypes.byref(fbv), 2) == pcs.PCS_ERR_INVALID
     assert b"unknown flag" in so.pcs_last_error()
     nulls = (ctypes.c_void_p * 2)(arr[0], None)
-    assert so.pcs_pages_validate_host(nulls, 4096, 2, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID
+    assert so.pcs_pages_validate_host_ex(nulls, 4096, 2, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_ERR_INVALID

@@ -42,3 +42,47 @@ def test_bench_line_and_sweep():
         assert e["steps"] == 3 and e["warmup"] == 1
     # config-2 entries ran on the headline's batch (resident, not re-allocated)
     assert [e["pages"] for e in d["sweep"] if e["config"] == 2] == [65536, 65536]
+
+
+def _one_line(r):
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_config1_leg_on_the_real_file():
+    """BASELINE configs[0]: the GPU CLI writes and stamps the 1 GiB file, the
+    reference's own xxHash validates every page on one thread, the repo's C
+    restatement re-digests them, and the CLI's --scan scrubs the file: all
+    must agree (tools/page_checksum_tool.cpp:94-105, page.cpp:25-31)."""
+    d = _one_line(subprocess.run([sys.executable, "bench.py", "--config", "1", "--cpu-seconds", "1",
+                                  "--no-all-cores"], cwd=ROOT, capture_output=True, text=True, timeout=300))
+    assert "error" not in d, d
+    one = d["cpu_baseline"]
+    assert one["kind"] == "reference" and one["cores"] == 1 and one["value"] > 0
+    assert one["pages_failed"] == 0
+    assert d["cpu_port"]["pages_failed"] == 0 and d["cpu_port"]["value"] > 0
+    assert d["cli_scan"]["rc"] == 0, d["cli_scan"]
+    assert d["cpu_all_cores"] is None
+    assert not os.listdir(os.path.join(ROOT, ".bench_tmp")), "config-1 file left behind"
+
+
+def test_bench_line_survives_failing_config1():
+    env = dict(os.environ, PCS_BENCH_FAIL_CONFIG1="1")
+    d = _one_line(subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--pages-per-gpu",
+                                  "65536", "--no-sweep", "--host-inclusive"], cwd=ROOT, env=env,
+                                 capture_output=True, text=True, timeout=300))
+    assert "PCS_BENCH_FAIL_CONFIG1" in d["config1_error"]
+    assert d["cpu_baseline"] is None
+    assert d["roofline"]["frac"] > 0 and d["parity"]["mismatches"] == 0
+    assert d["host_inclusive"]["direct_pinned_digests_match_device"]
+
+
+def test_bench_wall_budget_skips_optional_legs():
+    d = _one_line(subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--pages-per-gpu",
+                                  "65536", "--sweep-scale", "16", "--wall-budget", "0"], cwd=ROOT,
+                                 capture_output=True, text=True, timeout=300))
+    assert "wall budget" in d["config1_skipped"]
+    assert [e["key"] for e in d["sweep"]] == SWEEP_KEYS and all("skipped" in e for e in d["sweep"])
+    assert d["roofline"]["frac"] > 0

@@ -557,7 +557,7 @@ def test_host_direct_pinned_path(algo):
     ptrs = np.arange(n, dtype=np.uint64) * np.uint64(P) + np.uint64(pinned.data_ptr())
     ok = np.empty(n, dtype=np.uint8)
     fb = ctypes.c_uint64(0)
-    rc = pcs.lib().pcs_pages_validate_host(ptrs.ctypes.data, P, n, algo, ok.ctypes.data, ctypes.byref(fb), 0)
+    rc = pcs.lib().pcs_pages_validate_host(ptrs.ctypes.data, P, n, algo, ok.ctypes.data, ctypes.byref(fb))
     assert rc == 0 and fb.value == 777 and int((ok == 0).sum()) == 1
 
 

@@ -218,8 +218,8 @@ int bulk(bool stamp, const char* path, const char* size_s) {
         // scrub (a long-running service pays it once)
         std::memset(buf[0], 0, (size_t)P);
         const void* one = buf[0];
-        if (pcs_batch_submit(batch[0], stamp ? PCS_BATCH_DIGEST : PCS_BATCH_VALIDATE, &one, P, 1, PCS_XXH3_64,
-                             PCS_FLAG_NONE) == PCS_OK)
+        if (pcs_batch_submit(batch[0], stamp ? PCS_BATCH_DIGEST : PCS_BATCH_VALIDATE, &one, P, 1,
+                             PCS_XXH3_64) == PCS_OK)
             (void)pcs_batch_wait(batch[0]);
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -240,7 +240,7 @@ int bulk(bool stamp, const char* path, const char* size_s) {
         ptrs[s].resize(cnt);
         for (uint64_t i = 0; i < cnt; ++i) ptrs[s][i] = b + i * P;
         if (pcs_batch_submit(batch[s], stamp ? PCS_BATCH_STAMP : PCS_BATCH_VALIDATE, ptrs[s].data(), P, cnt,
-                             PCS_XXH3_64, PCS_FLAG_NONE)) {
+                             PCS_XXH3_64)) {
             rc = 1;
             break;
         }
