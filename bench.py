@@ -756,17 +756,12 @@ def main():
     drill = w.corruption_drill() if rank == 0 else None
     time.sleep(PHASE_GAP_S)
     # Optional legs, each guarded: a failure is recorded under its key and the
-    # headline line (roofline, parity, drill) still prints.  Config 1 runs first
-    # since cpu_baseline belongs to the contract line; the sweep is last and
-    # skips entries past the wall budget.
-    c1 = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        all_s = None if args.no_all_cores else min(args.cpu_seconds, 5.0)
-        need = args.cpu_seconds + (all_s or 0) + 3.0 + 30.0  # + port leg + gen/scan/warm margin
-        if time.perf_counter() + need > deadline:
-            c1 = {"skipped": f"bench wall budget: {deadline - time.perf_counter():.0f} s left, ~{need:.0f} s needed"}
-        else:
-            c1 = guarded("config1", config1, args.cpu_seconds, all_s)
+    # headline line (roofline, parity, drill) still prints.  The sweep runs
+    # before config 1: with config 1 first (its CLI processes initialise the
+    # GPU beside this one), one box measured config 3 XXH3 at 0.82 instead of
+    # 0.89 (gpurun_out r03a, profiles/r03a_sweep.json).  Sweep entries past
+    # the wall budget are skipped, and config 1 is skipped when the time left
+    # cannot hold it.
     hostinc = None
     if args.host_inclusive and rank == 0:
         hostinc = guarded("host_inclusive", host_inclusive, w) if time.perf_counter() < deadline else \
@@ -775,6 +770,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep_entries = guarded("sweep", sweep, dev, args.sweep_steps, args.sweep_warmup,
                                 head=w if algo == 0 else None, scale=max(1, args.sweep_scale), deadline=deadline)
+    c1 = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        all_s = None if args.no_all_cores else min(args.cpu_seconds, 5.0)
+        need = args.cpu_seconds + (all_s or 0) + 3.0 + 30.0  # + port leg + gen/scan/warm margin
+        if time.perf_counter() + need > deadline:
+            c1 = {"skipped": f"bench wall budget: {deadline - time.perf_counter():.0f} s left, ~{need:.0f} s needed"}
+        else:
+            c1 = guarded("config1", config1, args.cpu_seconds, all_s)
 
     if rank == 0:
         achieved = w.algorithmic_bytes(args.mode) / avg_launch / 1e9

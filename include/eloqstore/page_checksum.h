@@ -39,6 +39,27 @@ bool ValidateChecksum(std::string_view blob);
 // Hash variant for the batched forms (the reference path is always XXH3).
 enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 
+// Batch-size policy for the call sites.  A GPU batch pays
+// a fixed launch + completion cost before any byte is hashed (~17 µs for one
+// page) while the reference's CPU loop pays per page, so small batches stay on
+// the reference's own per-page ValidateChecksum / SetChecksum (page.cpp:18-31):
+// the 6-page scan prefetch (types.h:31, scan_task.cpp:215), short overflow
+// reads (task.cpp:136), the tail of a write batch.  The default is the measured
+// latency crossover of a zero-copy validate against one core running the
+// reference loop over the same scattered 4 KiB pool pages
+// (tests/cpp/integration_harness.cpp.in --crossover).
+inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(384) << 10;
+inline bool GpuChecksumPays(size_t n_pages, size_t page_size, size_t min_bytes = kGpuChecksumMinBatchBytes) {
+    return n_pages * page_size >= min_bytes;
+}
+
+// Manifest records (ManifestBuilder::CalcChecksum, root_meta.cpp:150-174):
+// the host-memory ManifestChecksum crosses PCIe once and runs three launches,
+// so only records of at least this many bytes (snapshots, large mapping logs)
+// pay on the GPU; smaller ones keep the reference loop.  Measured crossover,
+// same harness.
+inline constexpr size_t kGpuManifestMinBytes = size_t(4) << 20;
+
 // Validates every page; ok_out[i] = 1 if page i's stored digest matches.
 // Returns the index of the first corrupted page, or pages.size() if all match
 // (the reference loop stops at the first failure, async_io_manager.cpp:357-363;

@@ -73,9 +73,12 @@ def compile_tu(out: str, syntax_only: bool = False) -> subprocess.CompletedProce
     else:
         lib = os.path.join(ROOT, "eloqstore_amd")
         orc = os.path.join(ROOT, "oracle")
-        cmd += ["-o", out, f"-L{lib}", "-leloqstore_pcs", f"-L{orc}", "-loracle",
+        # page.cpp's CPU SetChecksum/ValidateChecksum stand-ins hash with the
+        # reference's own xxhash.c (oracle/_ref, built by `make -C oracle ref`)
+        cmd += ["-o", out, f"-L{lib}", "-leloqstore_pcs", f"-L{orc}", "-loracle", f"-L{orc}/_ref", "-lxxhash_ref",
                 "-Wl,-rpath-link,/opt/rocm/lib",
-                "-Wl,-rpath,$ORIGIN/../../eloqstore_amd", "-Wl,-rpath,$ORIGIN/../../oracle"]
+                "-Wl,-rpath,$ORIGIN/../../eloqstore_amd", "-Wl,-rpath,$ORIGIN/../../oracle",
+                "-Wl,-rpath,$ORIGIN/../../oracle/_ref"]
     return subprocess.run(cmd, capture_output=True, text=True)
 
 

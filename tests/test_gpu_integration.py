@@ -5,7 +5,13 @@ page.h exists; the binary travels with the tree).
 The binary drives the ReadPages validate loop (sync and async, registered pool
 and heap pages, a corrupted page at index 77, skip_verify_checksum), and the
 WritePage / FlushBatchPages stamping in append and non-append mode, with the
-CPU oracle checking every stamped header."""
+CPU oracle checking every stamped header.  Both sides of the batch-size gate
+(kGpuChecksumMinBatchBytes) run: a 128-page read batch and a 256-page write
+batch on the GPU, a 6-page scan-prefetch batch (types.h:31) and a 10-page
+write tail on page.cpp's CPU loop, told apart by call counters and
+pcs_counter().  Manifest records below and above kGpuManifestMinBytes go
+through Finalize, ValidateChecksum and the replay check (replayer.cpp:92),
+with a flipped byte rejected."""
 import os
 import subprocess
 
@@ -23,4 +29,9 @@ def test_integration_snippets_run():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "integration ok" in r.stdout
     assert "read path source=registered: ok" in r.stdout and "read path source=heap: ok" in r.stdout
-    assert "write path append=1: 256 pages stamped" in r.stdout
+    assert "write path append=1: 256 pages stamped (GPU batch)" in r.stdout
+    assert "write path append=1: 10 pages stamped (reference loop)" in r.stdout
+    assert "write path append=0: 40 pages stamped (reference loop)" in r.stdout
+    assert "6-page scan batch on the reference loop" in r.stdout
+    assert r.stdout.count("manifest record") == 2
+    assert "(reference loop)" in r.stdout.split("manifest record")[1] and "(GPU)" in r.stdout.split("manifest record")[2]

@@ -28,7 +28,7 @@ LIB = os.path.join(ROOT, "eloqstore_amd", "libeloqstore_pcs.so")
 def test_every_snippet_is_used():
     blocks = gi.snippets(open(gi.DOC).read())
     assert set(blocks) == {"read_validate", "read_validate_async", "pool_extend", "write_page_stamp",
-                           "flush_batch_stamp"}
+                           "flush_batch_stamp", "manifest_calc_checksum", "replay_validate"}
     src = gi.render(open(gi.DOC).read(), open(gi.TEMPLATE).read())
     assert '#include "storage/page.h"' in src and not gi._MARK.search(src)
     for body in blocks.values():
@@ -46,10 +46,16 @@ def test_snippets_link_against_library(tmp_path):
     r = gi.compile_tu(str(out), syntax_only=False)
     assert r.returncode == 0, r.stderr
     nm = subprocess.run(["nm", "-D", "--undefined-only", str(out)], capture_output=True, text=True).stdout
-    for sym in ("_ZN9eloqstore11SetChecksumESt17basic_string_viewIcSt11char_traitsIcEE",
-                "_ZN9eloqstore16ValidateChecksumESt17basic_string_viewIcSt11char_traitsIcEE",
-                "ValidateChecksums", "SetChecksums", "RegisterPagePool", "13ChecksumBatch14SubmitValidate"):
+    for sym in ("ValidateChecksums", "SetChecksums", "RegisterPagePool", "13ChecksumBatch14SubmitValidate",
+                "ManifestChecksum"):
         assert sym in nm, f"{sym} not bound from libeloqstore_pcs.so"
+    # page.cpp's single-page CPU functions stay the store's own (INTEGRATION.md
+    # §2.4): the harness defines them, so the small-batch branches never reach
+    # the library's single-page GPU symbols
+    defined = subprocess.run(["nm", "--defined-only", str(out)], capture_output=True, text=True).stdout
+    for sym in ("_ZN9eloqstore11SetChecksumESt17basic_string_viewIcSt11char_traitsIcEE",
+                "_ZN9eloqstore16ValidateChecksumESt17basic_string_viewIcSt11char_traitsIcEE"):
+        assert sym in defined and sym not in nm
     lib_syms = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
     for line in nm.splitlines():
         name = line.split()[-1]
