@@ -40,25 +40,29 @@ bool ValidateChecksum(std::string_view blob);
 enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 
 // Batch-size policy for the call sites.  A GPU batch pays
-// a fixed launch + completion cost before any byte is hashed (~17 µs for one
-// page) while the reference's CPU loop pays per page, so small batches stay on
-// the reference's own per-page ValidateChecksum / SetChecksum (page.cpp:18-31):
-// the 6-page scan prefetch (types.h:31, scan_task.cpp:215), short overflow
-// reads (task.cpp:136), the tail of a write batch.  The default is the measured
-// latency crossover of a zero-copy validate against one core running the
-// reference loop over the same scattered 4 KiB pool pages
-// (tests/cpp/integration_harness.cpp.in --crossover).
-inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(384) << 10;
+// a fixed launch + completion cost before any byte is hashed (~21 µs for one
+// page) while the reference's CPU loop pays per page (~0.6 µs per cache-cold
+// 4 KiB page), so small batches stay on the reference's own per-page
+// ValidateChecksum / SetChecksum (page.cpp:18-31): the 6-page scan prefetch
+// (types.h:31, scan_task.cpp:215), short overflow reads (task.cpp:136), the
+// tail of a write batch.  Defaults are the measured latency crossovers of one
+// call against one core running the reference loop over the same scattered
+// 4 KiB pool pages (integration_snippets --crossover):
+//   registered pool (RegisterPagePool, zero-copy): GPU faster from 48 pages;
+//   unregistered pages (gathered into staging):    GPU faster from 192 pages.
+inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(192) << 10;
+inline constexpr size_t kGpuChecksumMinBatchBytesStaged = size_t(768) << 10;
 inline bool GpuChecksumPays(size_t n_pages, size_t page_size, size_t min_bytes = kGpuChecksumMinBatchBytes) {
     return n_pages * page_size >= min_bytes;
 }
 
 // Manifest records (ManifestBuilder::CalcChecksum, root_meta.cpp:150-174):
-// the host-memory ManifestChecksum crosses PCIe once and runs three launches,
-// so only records of at least this many bytes (snapshots, large mapping logs)
-// pay on the GPU; smaller ones keep the reference loop.  Measured crossover,
-// same harness.
-inline constexpr size_t kGpuManifestMinBytes = size_t(4) << 20;
+// the host-memory ManifestChecksum copies the record over PCIe and runs three
+// launches (~54 µs at 64 KiB), so only records from this size on (snapshots,
+// large mapping logs) are faster on the GPU; smaller ones keep the reference
+// loop.  Measured crossover, same harness: 6 MiB (259 vs 239 µs; 64 MiB:
+// 2.8 ms on one core, 1.44 ms on the GPU).
+inline constexpr size_t kGpuManifestMinBytes = size_t(6) << 20;
 
 // Validates every page; ok_out[i] = 1 if page i's stored digest matches.
 // Returns the index of the first corrupted page, or pages.size() if all match
