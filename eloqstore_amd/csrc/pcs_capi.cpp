@@ -63,9 +63,11 @@ int pages_common(int mode, const void* d_pages, uint64_t P, uint64_t n, int algo
     if (mode == 0 && n && !d_out) return fail(PCS_ERR_INVALID, "d_digests is null");
     if (mode == 1 && n && !d_ok) return fail(PCS_ERR_INVALID, "d_ok is null");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (n == 0 && !d_first_bad) return PCS_OK;
-    // d_first_bad is written by the validate kernels themselves (a leased
-    // self-resetting slot, pcs_kernels.hip BadSlots): no fill launch
+    if (d_first_bad) {
+        hipError_t e = hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(first_bad)");
+    }
+    if (n == 0) return PCS_OK;
     auto* fb = reinterpret_cast<unsigned long long*>(d_first_bad);
     return finish(pcs::run_pages(mode, algo, static_cast<const uint8_t*>(d_pages), P, n, d_out, d_ok, fb, s),
                   "page kernel launch");
@@ -79,7 +81,11 @@ int desc_common(int mode, const void* d_base, const uint64_t* d_off, const uint3
     if (mode == 0 && n && !d_out) return fail(PCS_ERR_INVALID, "d_digests is null");
     if (mode == 1 && n && !d_ok) return fail(PCS_ERR_INVALID, "d_ok is null");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (n == 0 && !d_first_bad) return PCS_OK;
+    if (d_first_bad) {
+        hipError_t e = hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(first_bad)");
+    }
+    if (n == 0) return PCS_OK;
     return finish(pcs::run_desc(mode, algo, static_cast<const uint8_t*>(d_base), d_off, d_len, n, skip, seed, d_out,
                                 d_ok, reinterpret_cast<unsigned long long*>(d_first_bad), s),
                   "descriptor kernel launch");

@@ -49,7 +49,7 @@ namespace pcs {
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   FirstBad first_bad, uint64_t win) {
+                                                   unsigned long long* first_bad) {
     static_assert(MODE != kStamp, "stamps run as digest + k_scatter_stamp");
     __shared__ uint64_t tile_h[16];
     __shared__ uint8_t tile_ok[16];
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t t = remap ? xcd_tile_win(t0, ntiles, win) : t0;
+        const uint64_t t = remap ? xcd_tile(t0, ntiles) : t0;
         const uint64_t pg = t * 16 + grp;
         if (pg < n) {
             const uint8_t* page = pages + pg * (uint64_t)P;
@@ -86,7 +86,6 @@ __global__ __launch_bounds__(256) void k_xxh3_fixed(const uint8_t* __restrict__ 
         }
         __syncthreads();
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // Split pages (P = 8, 16, 32 or 64 KiB): G = P / 4096 groups share a page,
@@ -163,7 +162,7 @@ __device__ __forceinline__ void xxh3_split_tile(const Xxh3Lane& L, PageAt page_a
 template <int P, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ pages, uint64_t n,
                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                   FirstBad first_bad) {
+                                                   unsigned long long* first_bad) {
     constexpr int PPB = 16 / (P / 4096);  // pages per 256-thread block
     __shared__ uint64_t S[64 * 8];        // block sums per accumulator pair (even, odd)
     __shared__ uint64_t C[16];            // first input word of each slice (the previous block's carry)
@@ -197,7 +196,6 @@ __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ 
         // the next tile's writes to S / tile_h wait for everyone's reads here
         __syncthreads();
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // Fixed stride, run-time page size.  BODY 0 / 1: the chunked body one block
@@ -206,7 +204,7 @@ __global__ __launch_bounds__(256) void k_xxh3_split(const uint8_t* __restrict__ 
 template <int MODE, bool NT, int BODY>
 __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                     uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                    FirstBad first_bad) {
+                                                    unsigned long long* first_bad) {
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t ntiles = (n + 15) / 16;
     const bool remap = gridDim.x == ntiles;
@@ -220,7 +218,6 @@ __global__ __launch_bounds__(256) void k_xxh3_stride(const uint8_t* __restrict__
                                        : xxh3_page_rt<NT>(page, P, L, stored);
         if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // Page list: page pg is the absolute address ptrs[pg], all of size P
@@ -426,7 +423,7 @@ template <int MODE, bool NT, int ADDR, int DEPTH, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                        const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                       FirstBad first_bad) {
+                                                       unsigned long long* first_bad) {
     __shared__ __attribute__((aligned(16))) u32x4 lds[WPB][16][16];  // [wave][page slot][16 B slot]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = lane >> 4, t = lane & 15;        // loader role
@@ -537,7 +534,6 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
             if (q == 0) emit(MODE, hp, h, stored, const_cast<uint8_t*>(hptr), out, ok, first_bad);
         }
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // Pages off the 64-byte-piece shape (P % 64 != 0 or 8-byte-aligned only): one
@@ -547,7 +543,7 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
 template <int MODE>
 __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict__ pages, uint32_t P, uint64_t n,
                                                      uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                     FirstBad first_bad) {
+                                                     unsigned long long* first_bad) {
     const int a = threadIdx.x & 3;
     const uint64_t ntiles = (n + 63) / 64;
     const bool remap = gridDim.x == ntiles;
@@ -559,7 +555,6 @@ __global__ __launch_bounds__(256) void k_xxh64_stride(const uint8_t* __restrict_
         const uint64_t h = xxh64_page<false>(page, P, a, stored);
         if (a == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, first_bad);
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // long raw-range shape (k_xxh3_long, below); the lane kernel skips these
@@ -690,7 +685,7 @@ template <int MODE>
 __device__ __forceinline__ void generic_one(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                             const uint32_t* __restrict__ len, uint64_t i, int algo, uint64_t seed,
                                             int skip, uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                            FirstBad first_bad) {
+                                            unsigned long long* first_bad) {
     const uint64_t o = off[i];
     const uint32_t L = len[i];
     const uint8_t* p = base + o;
@@ -731,11 +726,11 @@ __device__ __forceinline__ void generic_one(const uint8_t* __restrict__ base, co
 // loop: +1.1 % digest / +0.8 % validate on config 3
 // (profiles/r02/desc_tp_lab.txt, list 1 vs 0).  Loading the next tile's
 // descriptors ahead with 2 or 4 tiles per workgroup was slower (-0.4..-2.7 %).
-template <int MODE, bool NT, bool B4, bool SD = false>
+template <int MODE, bool NT, bool B4>
 __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, uint64_t n,
                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                  FirstBad first_bad) {
+                                                  unsigned long long* first_bad) {
     __shared__ uint64_t tile_h[16];
     __shared__ uint8_t tile_st[16];  // 0 bad, 1 good, 2 not this kernel's page
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
@@ -748,28 +743,9 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
     const int grp = threadIdx.x >> 4;
     const uint64_t pg = t * 16 + grp;
     uint8_t st = 2;
-    uint64_t o = 0;
-    uint32_t P = 0;
-    if constexpr (SD) {
-        // SD (PCS_TUNE_SCALAR_DESC): the wave's 4 descriptors (32 + 16 B,
-        // wave-uniform address) as scalar loads, then a per-group select, in
-        // place of each group's own vector loads of its descriptor
-        const uint64_t pw = t * 16 + 4 * (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int gi = grp & 3;
-        if (pw + 4 <= n) {
-            const uint64_t o0 = off[pw], o1 = off[pw + 1], o2 = off[pw + 2], o3 = off[pw + 3];
-            const uint32_t l0 = len[pw], l1 = len[pw + 1], l2 = len[pw + 2], l3 = len[pw + 3];
-            o = gi == 0 ? o0 : gi == 1 ? o1 : gi == 2 ? o2 : o3;
-            P = gi == 0 ? l0 : gi == 1 ? l1 : gi == 2 ? l2 : l3;
-        } else if (pg < n) {
-            o = off[pg];
-            P = len[pg];
-        }
-    } else if (pg < n) {
-        o = off[pg];
-        P = len[pg];
-    }
     if (pg < n) {
+        const uint64_t o = off[pg];
+        const uint32_t P = len[pg];
         if (xxh3_fast_ok(o, P)) {
             const uint8_t* page = base + o;
             uint64_t stored = 0;
@@ -823,7 +799,6 @@ __global__ __launch_bounds__(256) void k_xxh3_desc(const uint8_t* __restrict__ b
                 }
         }
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // One lane per range.  SKIP = 8 applies the page convention (hash [8, len),
@@ -835,14 +810,13 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ len, uint64_t n, int algo,
                                                      uint64_t seed, int skip, int filter, uint64_t* __restrict__ out,
-                                                     uint8_t* __restrict__ ok, FirstBad first_bad) {
+                                                     uint8_t* __restrict__ ok, unsigned long long* first_bad) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (filter == 1 && algo == 1 && xxh64_lines_ok(off[i], len[i])) continue;
         if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
         generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
     }
-    if constexpr (MODE == kValidate) finish_first_bad(first_bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -1372,95 +1346,6 @@ struct ScratchLease {
     }
 };
 
-// Self-resetting first_bad accumulators (FirstBad, xxh3_page.h).  A slot is
-// {acc = UINT64_MAX, done = 0} whenever no launch uses it: set once when its
-// chunk of slots is allocated and put back by the last block of every call.
-// Leases are fenced like ScratchPool buffers (an event recorded behind the
-// call's launches), so calls on other streams or threads never share a slot
-// in flight.  This replaces a fill launch (hipMemsetAsync of the caller's
-// word, 5.2 us per call in round 2) in front of every validate call.
-class BadSlots {
-public:
-    hipError_t acquire(unsigned long long** out, int* id) {
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e != hipSuccess) return e;
-        std::lock_guard<std::mutex> lk(mu_);
-        for (size_t i = 0; i < slots_.size(); ++i) {
-            Slot& b = slots_[i];
-            if (b.dev != dev || b.busy) continue;
-            if (b.done) {
-                const hipError_t q = hipEventQuery(b.done);
-                if (q == hipErrorNotReady) continue;
-                if (q != hipSuccess) return q;
-            }
-            b.busy = true;
-            *out = b.p;
-            *id = (int)i;
-            return hipSuccess;
-        }
-        // a new chunk of kChunk slots, each {UINT64_MAX, 0}
-        void* mem = nullptr;
-        if ((e = hipMalloc(&mem, kChunk * 16)) != hipSuccess) return e;
-        if ((e = hipMemcpy(mem, reset_image(), kChunk * 16, hipMemcpyHostToDevice)) != hipSuccess) {
-            (void)hipFree(mem);
-            return e;
-        }
-        const size_t first = slots_.size();
-        for (int k = 0; k < kChunk; ++k) {
-            Slot b;
-            b.dev = dev;
-            b.p = static_cast<unsigned long long*>(mem) + 2 * k;
-            slots_.push_back(b);
-        }
-        slots_[first].busy = true;
-        *out = slots_[first].p;
-        *id = (int)first;
-        return hipSuccess;
-    }
-    // After the call's launches were enqueued on s.  A call whose launches did
-    // not all start leaves the slot counted part-way: it is reset in stream
-    // order before the slot is handed out again.
-    hipError_t release(int id, hipStream_t s, bool launched) {
-        std::lock_guard<std::mutex> lk(mu_);
-        Slot& b = slots_[(size_t)id];
-        hipError_t e = hipSuccess;
-        if (!launched) e = hipMemcpyAsync(b.p, reset_image(), 16, hipMemcpyHostToDevice, s);
-        if (!b.done && e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
-        if (b.done) {
-            const hipError_t r = hipEventRecord(b.done, s);
-            if (e == hipSuccess) e = r;
-        }
-        b.busy = false;
-        return e;
-    }
-
-private:
-    static constexpr int kChunk = 64;
-    static const unsigned long long* reset_image() {
-        static const std::vector<unsigned long long> img = [] {
-            std::vector<unsigned long long> a(2 * kChunk, 0);
-            for (int k = 0; k < kChunk; ++k) a[2 * k] = ~0ull;
-            return a;
-        }();
-        return img.data();
-    }
-    struct Slot {
-        unsigned long long* p = nullptr;
-        hipEvent_t done = nullptr;
-        int dev = 0;
-        bool busy = false;
-    };
-    std::mutex mu_;
-    std::vector<Slot> slots_;
-};
-BadSlots g_bad_slots;
-
-FirstBad with_target(FirstBad fb, unsigned blocks) {
-    fb.target = blocks;
-    return fb;
-}
-
 bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) == 0; }
 
 }  // namespace
@@ -1469,7 +1354,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 25;
+constexpr int kTuneKeys = 22;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1480,9 +1365,8 @@ constexpr int kTuneKeys = 25;
 // 20 4 KiB-aligned descriptor steps (+-0.2 %, aligned_steps_lab.txt), 21 the
 // descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt).
 // Setting one fails.
-constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
-                                      true,  false, true,  false, true,  true,  true,  true,  true,  true,  false,
-                                      false, false};
+constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false,
+                                      true,  false, true,  false, true,  false, true,  true,  true,  true,  true,  true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1495,10 +1379,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4,
                                           /*retired*/ 0, /*retired*/ 0, /*retired*/ 0, /*retired*/ 0,
                                           /*retired*/ 0,
-                                          /*retired*/ 0,
-                                          /*validate first_bad: 1 leased self-resetting slot, 0 fill launch*/ 1,
-                                          /*fixed XXH3 kernel: XCD tile window in tiles (0 = whole batch)*/ 0,
-                                          /*descriptor XXH3 kernel: wave-uniform scalar descriptor loads*/ 0};
+                                          /*retired*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1528,30 +1409,19 @@ bool split_pages(uint64_t P) {
     return split > 0 && P >= (uint64_t)split && P >= 8192 && P <= 65536 && (P & (P - 1)) == 0;
 }
 bool rt_batch4() { return g_tune[8].load(std::memory_order_relaxed) != 0; }
-uint64_t xcd_window() { return (uint64_t)g_tune[23].load(std::memory_order_relaxed); }
-bool scalar_desc() { return g_tune[24].load(std::memory_order_relaxed) != 0; }
 
 // XXH64 LDS kernel launch with the segment depth from PCS_TUNE_XXH64_LAYOUT
 // (0 or 1 = default depth, 2/3/4 = depth 1/2/4) and the waves per workgroup
 // from PCS_TUNE_XXH64_WAVES.
-unsigned xxh64_lds_grid(unsigned grid, uint64_t n) {
-    const int64_t wpb = g_tune[15].load(std::memory_order_relaxed);
-    if (wpb == 1 || wpb == 2)  // one workgroup per 16 * wpb pages, every tile covered once
-        return (unsigned)std::min<uint64_t>((n + 16 * wpb - 1) / (16 * wpb), 0x7FFFFFFFull);
-    return grid;
-}
-
-// `later` = blocks of launches that follow this one in the same call (their
-// blocks finish the call's first_bad count).
 template <int MODE, bool NT, int ADDR>
 void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                      uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, FirstBad fb0, unsigned later = 0) {
+                      uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, unsigned long long* fb) {
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
     const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
     const int64_t wpb = g_tune[15].load(std::memory_order_relaxed);
-    const FirstBad fb = with_target(fb0, xxh64_lds_grid(grid, n) + later);
     if (wpb == 1 || wpb == 2) {
-        const unsigned g = xxh64_lds_grid(grid, n);
+        // one workgroup per 16 * wpb pages, every tile covered once
+        const unsigned g = (unsigned)std::min<uint64_t>((n + 16 * wpb - 1) / (16 * wpb), 0x7FFFFFFFull);
 #define LW(D, W) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D, W>), dim3(g), dim3(64 * W), 0, s, base, off, len, P, n, out, ok, fb)
         if (wpb == 1) {
             if (depth == 1) LW(1, 1);
@@ -1574,9 +1444,8 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
 
 template <int MODE, bool NT>
 hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint64_t* out, uint8_t* ok,
-                             FirstBad fb0, hipStream_t s) {
+                             unsigned long long* fb, hipStream_t s) {
     const unsigned grid = page_grid(n, kBlock / 16, 1, P);  // kBlock/16 = one 16-page tile per block
-    FirstBad fb = with_target(fb0, grid);
     if (P % 256 != 0) {  // off the chunk grid: the any-size body
         hipLaunchKernelGGL((k_xxh3_stride<MODE, NT, 2>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok,
                            fb);
@@ -1594,7 +1463,6 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
         const uint64_t ppb = 16 / (P / 4096);
         const uint64_t need = (n + ppb - 1) / ppb;
         const unsigned g = (unsigned)std::min<uint64_t>(need, 0x7FFFFFFFull);
-        fb = with_target(fb0, g);
         switch (P) {
 #define CASE(SZ) \
     case SZ: hipLaunchKernelGGL((k_xxh3_split<SZ, MODE, NT>), dim3(g), dim3(kBlock), 0, s, pages, n, out, ok, fb); break;
@@ -1606,8 +1474,7 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
     switch (P) {
 #define CASE(SZ)                                                                                             \
     case SZ:                                                                                                 \
-        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb, \
-                           xcd_window());                                                                    \
+        hipLaunchKernelGGL((k_xxh3_fixed<SZ, MODE, NT>), dim3(grid), dim3(kBlock), 0, s, pages, n, out, ok, fb);     \
         break;
         CASE(256) CASE(512) CASE(1024) CASE(2048) CASE(4096) CASE(8192) CASE(16384) CASE(32768) CASE(65536)
 #undef CASE
@@ -1627,7 +1494,7 @@ hipError_t launch_xxh3_pages(uint64_t P, const uint8_t* pages, uint64_t n, uint6
 // Fixed-stride pages.  Shape checks are done by the caller (capi).
 template <int MODE>
 static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
-                             FirstBad fb, hipStream_t s) {
+                             unsigned long long* fb, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const bool aligned16 = ((uintptr_t)pages % 16) == 0;
     const bool aligned8 = ((uintptr_t)pages % 8) == 0;
@@ -1670,8 +1537,7 @@ static hipError_t pages_impl(int algo, const uint8_t* pages, uint64_t P, uint64_
             return hipGetLastError();
         }
         const unsigned grid = page_grid(n, kBlock / 4, 2, P);
-        hipLaunchKernelGGL((k_xxh64_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok,
-                           with_target(fb, grid));
+        hipLaunchKernelGGL((k_xxh64_stride<MODE>), dim3(grid), dim3(kBlock), 0, s, pages, (uint32_t)P, n, out, ok, fb);
         return hipGetLastError();
     }
     return hipErrorNotSupported;  // caller falls back to the descriptor path
@@ -1685,22 +1551,8 @@ __global__ void k_uniform_desc(uint64_t P, uint64_t n, uint64_t* __restrict__ of
     }
 }
 
-template <int MODE>
-static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
-                            int skip, uint64_t seed, uint64_t* out, uint8_t* ok, FirstBad fb, hipStream_t s);
-
-static hipError_t desc_dispatch(int mode, int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                                uint64_t n, int skip, uint64_t seed, uint64_t* out, uint8_t* ok, FirstBad fb,
-                                hipStream_t s) {
-    switch (mode) {
-        case kDigest: return desc_impl<kDigest>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
-        case kValidate: return desc_impl<kValidate>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
-        default: return desc_impl<kStamp>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
-    }
-}
-
-static hipError_t pages_dispatch(int mode, int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out,
-                                 uint8_t* ok, FirstBad fb, hipStream_t s) {
+hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
+                     unsigned long long* fb, hipStream_t s) {
     hipError_t e;
     switch (mode) {
         case kDigest: e = pages_impl<kDigest>(algo, pages, P, n, out, ok, fb, s); break;
@@ -1716,37 +1568,7 @@ static hipError_t pages_dispatch(int mode, int algo, const uint8_t* pages, uint6
     uint32_t* len = reinterpret_cast<uint32_t*>(off + n);
     hipLaunchKernelGGL(k_uniform_desc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, n, off, len);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return desc_dispatch(mode, algo, pages, off, len, n, 8, 0, out, ok, fb, s);
-}
-
-// A validate call's first_bad word (PCS_TUNE_FIRST_BAD): 1 = leased
-// self-resetting slot, the last block writes the caller's word (no extra
-// launch); 0 = the round-2 form, a fill launch (hipMemsetAsync) of the
-// caller's word in front of the kernels, which atomicMin into it directly.
-template <typename Run>
-static hipError_t with_first_bad(unsigned long long* fb_out, uint64_t n, hipStream_t s, Run run) {
-    if (!fb_out) return run(FirstBad(nullptr));
-    if (n == 0) return hipMemsetAsync(fb_out, 0xFF, 8, s);
-    if (g_tune[22].load(std::memory_order_relaxed) == 0) {
-        // the caller's word is the accumulator (no hand-off: out = nullptr)
-        const hipError_t e = hipMemsetAsync(fb_out, 0xFF, 8, s);
-        return e != hipSuccess ? e : run(FirstBad(fb_out, nullptr, 0));
-    }
-    unsigned long long* slot = nullptr;
-    int id = -1;
-    hipError_t e = g_bad_slots.acquire(&slot, &id);
-    if (e != hipSuccess) return e;
-    e = run(FirstBad(slot, fb_out, 0));
-    const hipError_t r = g_bad_slots.release(id, s, e == hipSuccess);
-    return e != hipSuccess ? e : r;
-}
-
-hipError_t run_pages(int mode, int algo, const uint8_t* pages, uint64_t P, uint64_t n, uint64_t* out, uint8_t* ok,
-                     unsigned long long* fb_out, hipStream_t s) {
-    if (mode != kValidate) fb_out = nullptr;
-    return with_first_bad(fb_out, n, s, [&](FirstBad fb) {
-        return pages_dispatch(mode, algo, pages, P, n, out, ok, fb, s);
-    });
+    return run_desc(mode, algo, pages, off, len, n, 8, 0, out, ok, fb, s);
 }
 
 hipError_t scratch_acquire(size_t bytes, void** out, int* id) { return g_scratch.acquire(bytes, out, id); }
@@ -1754,7 +1576,7 @@ hipError_t scratch_release(int id, hipStream_t s) { return g_scratch.release(id,
 
 template <int MODE>
 static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
-                            int skip, uint64_t seed, uint64_t* out, uint8_t* ok, FirstBad fb,
+                            int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* fb,
                             hipStream_t s) {
     if (n == 0) return hipSuccess;
     if constexpr (MODE == kStamp) {
@@ -1787,17 +1609,14 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             const uint64_t ntiles = (n + 15) / 16;
             if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
             const unsigned grid = (unsigned)ntiles;
-#define L(NT_, B4_, SD_) \
-    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_, SD_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, \
-                       with_target(fb, grid))
-            if (use_nt() && rt_batch4()) {
-                if (scalar_desc()) L(true, true, true);
-                else L(true, true, false);
-            } else if (use_nt()) {
-                L(true, false, false);
+#define L(NT_, B4_) \
+    hipLaunchKernelGGL((k_xxh3_desc<MODE, NT_, B4_>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, out, ok, fb)
+            if (use_nt()) {
+                if (rt_batch4()) L(true, true);
+                else L(true, false);
             } else {
-                if (rt_batch4()) L(false, true, false);
-                else L(false, false, false);
+                if (rt_batch4()) L(false, true);
+                else L(false, false);
             }
 #undef L
             // every page is the descriptor kernel's (fast body, any-size body,
@@ -1806,9 +1625,8 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             return hipGetLastError();
         } else {
             const unsigned grid = page_grid(n, kBlock / 4, 2);
-            const unsigned later = grid_for(n, kBlock, kBlocksPerCu);  // the generic pass below
-            if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, later);
-            else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, later);
+            if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
+            else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb);
             // Pages off the line shape (usually none) are left to the generic
             // lanes below.  A separate quad-per-page pass over the
             // descriptors for them cost 9.7 us per call on config 3 even when
@@ -1817,9 +1635,8 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         const unsigned grid = grid_for(n, kBlock, kBlocksPerCu);
-        const unsigned lds_blocks = xxh64_lds_grid(page_grid(n, kBlock / 4, 2), n);
         hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip,
-                           1, out, ok, with_target(fb, lds_blocks + grid));
+                           1, out, ok, fb);
         return hipGetLastError();
     }
     int filter = 0;
@@ -1833,7 +1650,7 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
     }
     const unsigned grid = grid_for(n, kBlock, kBlocksPerCu);
     hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(grid), dim3(kBlock), 0, s, base, off, len, n, algo, seed, skip,
-                       filter, out, ok, with_target(fb, grid));
+                       filter, out, ok, fb);
     return hipGetLastError();
 }
 
@@ -1878,11 +1695,12 @@ hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hip
 }
 
 hipError_t run_desc(int mode, int algo, const uint8_t* base, const uint64_t* off, const uint32_t* len, uint64_t n,
-                    int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* fb_out, hipStream_t s) {
-    if (mode != kValidate) fb_out = nullptr;
-    return with_first_bad(fb_out, n, s, [&](FirstBad fb) {
-        return desc_dispatch(mode, algo, base, off, len, n, skip, seed, out, ok, fb, s);
-    });
+                    int skip, uint64_t seed, uint64_t* out, uint8_t* ok, unsigned long long* fb, hipStream_t s) {
+    switch (mode) {
+        case kDigest: return desc_impl<kDigest>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
+        case kValidate: return desc_impl<kValidate>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
+        default: return desc_impl<kStamp>(algo, base, off, len, n, skip, seed, out, ok, fb, s);
+    }
 }
 
 hipError_t run_list(int mode, int algo, const uint64_t* ptrs, const uint64_t* host_ptrs, uint64_t P, uint64_t n,

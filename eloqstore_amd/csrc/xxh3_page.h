@@ -63,48 +63,8 @@ __device__ __forceinline__ void note_bad(unsigned long long* first_bad, uint64_t
         atomicMin(first_bad, (unsigned long long)idx);
 }
 
-// The first failing index of a validate call, with no fill launch in front of
-// it.  Blocks fold their failures into a device slot that is always left in
-// its reset state {UINT64_MAX, 0} (acc[0] = running minimum, acc[1] = blocks
-// finished); the block whose arrival completes the call's block count
-// (`target`, summed over every launch of the call) moves the minimum into the
-// caller's word and resets the slot.  All hand-offs are agent-scope atomics
-// (valid cross-XCD, MI355X_MICROARCH.md § visibility: "8-B agent atomics both
-// sides").  Slots are leased per call and fenced by events (pcs_kernels.hip
-// BadSlots), so concurrent calls never share one.
-struct FirstBad {
-    unsigned long long* acc = nullptr;
-    unsigned long long* out = nullptr;
-    unsigned target = 0;
-    FirstBad() = default;
-    __host__ __device__ FirstBad(decltype(nullptr)) {}
-    __host__ __device__ FirstBad(unsigned long long* a, unsigned long long* o, unsigned t) : acc(a), out(o), target(t) {}
-    __host__ __device__ explicit operator bool() const { return acc != nullptr; }
-};
-
-__device__ __forceinline__ void note_bad(const FirstBad& fb, uint64_t idx) { note_bad(fb.acc, idx); }
-
-// Called by every thread of the block once, after its last page (it
-// contains a workgroup barrier).  A block's atomics are complete (vmcnt
-// drained by every wave) before its lane 0 counts the block as done.
-__device__ __forceinline__ void finish_first_bad(const FirstBad& fb) {
-    if (!fb.out) return;  // uniform (kernel argument): no slot, or the caller's word is the accumulator
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned* done = reinterpret_cast<unsigned*>(fb.acc + 1);
-        const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == fb.target - 1) {
-            const unsigned long long m = __hip_atomic_exchange(fb.acc, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *fb.out = m;
-        }
-    }
-}
-
-template <typename FB>
 __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_t stored, uint8_t* page_w,
-                                     uint64_t* out, uint8_t* ok, FB first_bad) {
+                                     uint64_t* out, uint8_t* ok, unsigned long long* first_bad) {
     if (mode == kStamp) {
         st_nt(reinterpret_cast<uint64_t*>(page_w), h);
         if (out) st_nt(out + idx, h);
@@ -112,8 +72,7 @@ __device__ __forceinline__ void emit(int mode, uint64_t idx, uint64_t h, uint64_
         const bool good = (h == stored);
         st_nt(ok + idx, (uint8_t)(good ? 1 : 0));
         if (out) st_nt(out + idx, h);
-        if constexpr (!__is_same(FB, decltype(nullptr)))
-            if (!good && first_bad) note_bad(first_bad, idx);
+        if (!good && first_bad) note_bad(first_bad, idx);
     } else {
         st_nt(out + idx, h);
     }
@@ -476,17 +435,6 @@ __device__ __forceinline__ bool xxh3_group_ok(uint32_t P) { return P >= 249u; }
 __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t nb) {
     const uint64_t q = nb / 8, r = nb % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
-// Windowed form (PCS_TUNE_XCD_WINDOW): blocks are dispatched in roughly
-// increasing order, so window w = b / win of `win` consecutive blocks covers
-// tiles [w * win, (w + 1) * win), XCD-contiguous inside the window.  The chip's
-// live address span is then one window instead of the whole batch (eight
-// eighths streamed at once).  win = 0: the whole batch is one window.
-__device__ __forceinline__ uint64_t xcd_tile_win(uint64_t b, uint64_t nb, uint64_t win) {
-    if (win == 0 || win >= nb) return xcd_tile(b, nb);
-    const uint64_t w0 = b / win * win;
-    return w0 + xcd_tile(b - w0, nb - w0 < win ? nb - w0 : win);
 }
 
 }  // namespace pcs

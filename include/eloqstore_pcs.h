@@ -244,15 +244,6 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
  *                                     kernel (1, 2 or 4; 16 pages per wave)
- *   PCS_TUNE_FIRST_BAD            [1] validate calls' d_first_bad: 1 = written
- *                                     by the kernels' last block from a leased
- *                                     self-resetting slot (no extra launch);
- *                                     0 = a fill launch in front (round 2)
- *   PCS_TUNE_XCD_WINDOW           [0] fixed-size XXH3 kernel: XCD-contiguous
- *                                     tile order inside windows of this many
- *                                     16-page tiles (0 = one window, the batch)
- *   PCS_TUNE_SCALAR_DESC          [0] XXH3 descriptor kernel: a wave's four
- *                                     descriptors as scalar loads (1)
  * Keys 4, 5, 10, 12, 14 and 16-21 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -270,9 +261,6 @@ enum pcs_tune_key {
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_WAVES = 15,
-    PCS_TUNE_FIRST_BAD = 22,
-    PCS_TUNE_XCD_WINDOW = 23,
-    PCS_TUNE_SCALAR_DESC = 24,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

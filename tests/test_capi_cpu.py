@@ -119,7 +119,6 @@ def test_counters_and_tuning_defaults():
     assert pcs.get_tuning(5) == -1  # retired (in-place stamp width)
     assert pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES) == 8192
     assert pcs.get_tuning(pcs.TUNE_INLINE_LIST) == 1
-    assert pcs.get_tuning(pcs.TUNE_FIRST_BAD) == 1
 
 
 def test_skip_verify_flag_needs_no_gpu():

@@ -29,15 +29,12 @@ VARIANTS = {
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "x64_one_wave": {pcs.TUNE_XXH64_WAVES: 1},
     "x64_two_waves_depth4": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 4},
-    "first_bad_fill": {pcs.TUNE_FIRST_BAD: 0},
-    "xcd_window_7": {pcs.TUNE_XCD_WINDOW: 7},
-    "scalar_desc": {pcs.TUNE_SCALAR_DESC: 1},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = [k for k in range(1, 25) if pcs.get_tuning(k) >= 0]  # retired keys read -1
+    keys = [k for k in range(1, 16) if pcs.get_tuning(k) >= 0]  # retired keys read -1
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -157,7 +154,7 @@ def test_desc_mixed_with_leftovers(tuned, mode):
 
 def test_retired_tuning_keys_fail():
     """Keys of the variants retired in round 2 are refused, and read -1."""
-    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 25, 99):
+    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 22, 99):
         assert pcs.get_tuning(k) == -1
         with pytest.raises(pcs.PcsError):
             pcs.set_tuning(k, 1)
