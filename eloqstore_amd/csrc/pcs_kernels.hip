@@ -546,16 +546,33 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
 // programming.md rule 21): lane t of row r in instruction ii fetches chunk
 // (t - 4 ii) & 15 of page 4 ii + r, which lands in slot t, exactly where the
 // register-staged kernel stores chunk (slot - 4 ii) & 15; the quad reads are
-// unchanged.  Every instruction is issued with all 64 lanes (a lane with no
-// byte to fetch reads g_glds_pad), so each segment is exactly four vmcnt
-// events and `s_waitcnt vmcnt(4 (ahead))` retires precisely the segment about
-// to be hashed.
-__device__ __attribute__((aligned(16))) u32x4 g_glds_pad[16];
-
+// unchanged.  A lane with no byte to fetch is masked off (no traffic: config
+// 3's short pages would otherwise fetch padding), and an instruction no lane
+// of the wave needs is not issued; each segment's issued-instruction count is
+// wave-uniform (a ballot), so `s_waitcnt vmcnt(<instructions issued after
+// segment c>)` retires precisely the segment about to be hashed.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt field");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt takes an immediate: dispatch a wave-uniform count 0..12
+__device__ __forceinline__ void wait_vmcnt_dyn(uint32_t n) {
+    switch (n) {
+        case 0: wait_vmcnt<0>(); break;
+        case 1: wait_vmcnt<1>(); break;
+        case 2: wait_vmcnt<2>(); break;
+        case 3: wait_vmcnt<3>(); break;
+        case 4: wait_vmcnt<4>(); break;
+        case 5: wait_vmcnt<5>(); break;
+        case 6: wait_vmcnt<6>(); break;
+        case 7: wait_vmcnt<7>(); break;
+        case 8: wait_vmcnt<8>(); break;
+        case 9: wait_vmcnt<9>(); break;
+        case 10: wait_vmcnt<10>(); break;
+        case 11: wait_vmcnt<11>(); break;
+        default: wait_vmcnt<12>(); break;
+    }
 }
 
 template <int MODE, bool NT, int ADDR, int D, int WPB>
@@ -614,34 +631,52 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_glds(const uint8_t* __restri
             m = max(m, (uint32_t)__shfl_xor((int)m, 32));
             segs = __builtin_amdgcn_readfirstlane((m + 255) / 256);  // wave-uniform: scalar branches
         }
-        // every lane's source per instruction ii: chunk (t - 4 ii) & 15 of its
-        // row's page, or the pad when that page has no such byte
-        auto issue = [&](uint32_t c) {
+        // lane source per instruction ii: chunk (t - 4 ii) & 15 of its row's
+        // page; returns the instructions issued (wave-uniform)
+        auto issue = [&](uint32_t c) -> uint32_t {
+            uint32_t cnt = 0;
 #pragma unroll
             for (int ii = 0; ii < 4; ++ii) {
                 const uint32_t at = 256 * c + 16 * ((t - 4 * ii) & 15);
-                const void* src = at < lP[ii] ? static_cast<const void*>(lp[ii] + at)
-                                              : static_cast<const void*>(&g_glds_pad[t]);
-                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&lds[wv][c % D][4 * ii][0],
-                                                 16, 0, NT ? 2 : 0);
+                const bool need = at < lP[ii];
+                if (__builtin_amdgcn_ballot_w64(need) != 0) {
+                    ++cnt;
+                    if (need)
+                        __builtin_amdgcn_global_load_lds(lp[ii] + at,
+                                                         (__attribute__((address_space(3))) void*)&lds[wv][c % D][4 * ii][0],
+                                                         16, 0, NT ? 2 : 0);
+                }
             }
+            return __builtin_amdgcn_readfirstlane(cnt);
         };
+        uint32_t issued[D];  // instructions issued per in-flight segment (ring order)
         const int K = (int)(Ph / 64);
         uint64_t v = xxh64_init(a), stored = 0;
         u32x4 last = {0, 0, 0, 0};
         // the ring slot about to be refilled was read in the previous step:
         // those ds_reads are complete once their values were consumed
 #pragma unroll
+        for (int c = 0; c < D; ++c) issued[c] = 0;
+#pragma unroll
         for (int c = 0; c < D - 1; ++c)
-            if ((uint32_t)c < segs) issue(c);  // wave-uniform
+            if ((uint32_t)c < segs) issued[c] = issue(c);  // wave-uniform
         for (uint32_t c = 0; c < segs; ++c) {
-            const uint32_t ahead = min((uint32_t)(D - 1), segs - 1 - c);  // segments issued after c
-            if (c + D - 1 < segs) issue(c + D - 1);
-            // retire segment c: at most 4 * ahead later DMA instructions stay in flight
-            if (ahead >= 3) wait_vmcnt<12>();
-            else if (ahead == 2) wait_vmcnt<8>();
-            else if (ahead == 1) wait_vmcnt<4>();
-            else wait_vmcnt<0>();
+            if (c + D - 1 < segs) {
+                const uint32_t cnt = issue(c + D - 1);
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    if ((uint32_t)j == (c + D - 1) % D) issued[j] = cnt;
+            }
+            // retire segment c: the instructions of the segments after it stay in flight
+            uint32_t after = 0;
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+                if (c + j < segs) {
+#pragma unroll
+                    for (int x = 0; x < D; ++x)
+                        if ((uint32_t)x == (c + j) % D) after += issued[x];
+                }
+            wait_vmcnt_dyn(__builtin_amdgcn_readfirstlane(after));  // scalar branch: one wait runs
             __builtin_amdgcn_wave_barrier();
             const u32x4(*seg)[16] = lds[wv][c % D];
 #pragma unroll

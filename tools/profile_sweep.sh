@@ -4,6 +4,10 @@
 #   trace/  kernel trace + stats of the default N=1 bench run (headline + sweep)
 #   fetch/  --pmc FETCH_SIZE over a short run of the same entries
 #   write/  --pmc WRITE_SIZE over a short run (separate pass: gfx950 PMC slots)
+#   utcl/   --pmc UTCL1 address-translation counters (requests, hits, misses,
+#           multi-miss stalls) over the same short run: every box's record
+#           says whether large buffers (config 5, 32 GiB) miss in translation
+#           more than config 2's 4 GiB (VERDICT r02 Next #6)
 # Summarised by tools/summarize_sweep.py into profiles/<tag>_sweep.json.
 set -euo pipefail
 TAG=${1:-r02}
@@ -17,4 +21,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-f
     python3 bench.py $SHORT > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- \
     python3 bench.py $SHORT > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
+timeout -k 10 300 rocprofv3 --pmc TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_STALL_MULTI_MISS_sum \
+    -d "$OUT/utcl" -o utcl --output-format csv -- \
+    python3 bench.py $SHORT > "$OUT/bench_utcl.json" 2> "$OUT/bench_utcl.err"
 find "$OUT" -name "*.csv" | sort

@@ -85,6 +85,13 @@ def pmc_medians(path_glob):
     return {k: statistics.median(v) for k, v in by.items()}
 
 
+def pmc_by_counter(path_glob):
+    by = {}
+    for r in rows(path_glob):
+        by.setdefault((kname(r), grid(r)), {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: {c: statistics.median(v) for c, v in cs.items()} for k, cs in by.items()}
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     with open(os.path.join(src, "bench_trace.json")) as f:
@@ -92,6 +99,7 @@ def main():
     trace = rows(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
     fetch = pmc_medians(os.path.join(src, "fetch", "**", "*counter_collection.csv"))
     write = pmc_medians(os.path.join(src, "write", "**", "*counter_collection.csv"))
+    utcl = pmc_by_counter(os.path.join(src, "utcl", "**", "*counter_collection.csv"))
     segs = segments(trace)
 
     wanted = [{"key": "headline", "steps": bench["steps"], "frac": bench["roofline"]["frac"],
@@ -116,6 +124,15 @@ def main():
         rd = sum(fetch.get((k["kernel"], k["grid"]), float("nan")) for k in ks) * 1024 * 2
         wr = sum(write.get((k["kernel"], k["grid"]), float("nan")) for k in ks) * 1024
         traffic = rd + wr
+        tr = {}
+        for k in ks:
+            for c, v in utcl.get((k["kernel"], k["grid"]), {}).items():
+                tr[c] = tr.get(c, 0.0) + v
+        if tr.get("TCP_UTCL1_REQUEST_sum"):
+            tr["translation_miss_per_request"] = round(tr.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0)
+                                                       / tr["TCP_UTCL1_REQUEST_sum"], 6)
+            tr["translation_miss_per_MiB"] = round(tr.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0)
+                                                   / (w["alg"] / 2**20), 3)
         entries.append({
             "key": w["key"], "kernels": ks, "profile_launch_ms": round(t_ns / 1e6, 4),
             "bench_avg_launch_ms": w["avg_launch_ms"], "algorithmic_bytes_per_launch": w["alg"],
@@ -126,11 +143,13 @@ def main():
             "hbm_write_bytes_per_launch": None if wr != wr else round(wr),
             "traffic_bytes_per_launch": None if traffic != traffic else round(traffic),
             "traffic_over_algorithmic": None if traffic != traffic else round(traffic / w["alg"], 6),
+            "utcl1_per_launch": tr or None,
         })
     out = {
         "tag": tag,
         "how": "tools/profile_sweep.sh: rocprofv3 --kernel-trace over the default bench run (headline + sweep), "
-               "then --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate short runs; segments split on >20 ms idle "
+               "then --pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc TCP_UTCL1_* (address translation) in separate "
+               "short runs; segments split on >20 ms idle "
                "gaps; per entry the kernels launched >= steps times in its timed segment; launch time = sum of "
                "their median durations; read = FETCH_SIZE*1024*2 (gfx950 half-count), write = WRITE_SIZE*1024",
         "entries": entries,
@@ -142,7 +161,8 @@ def main():
     for e in entries:
         print(f"{e['key']:24s} prof {e.get('profile_launch_ms')} ms  frac_prof {e.get('frac_profile')}  "
               f"bench {e.get('frac_bench')}  agree {e.get('agree_within_2pct')}  "
-              f"traffic/alg {e.get('traffic_over_algorithmic')}")
+              f"traffic/alg {e.get('traffic_over_algorithmic')}  "
+              f"utcl1 miss/MiB {(e.get('utcl1_per_launch') or {}).get('translation_miss_per_MiB')}")
     print("wrote", dst)
 
 
