@@ -151,7 +151,6 @@ TUNE_XXH3_SPLIT_PAGES = 9
 TUNE_INLINE_LIST = 11
 TUNE_MANIFEST_WIDE = 13
 TUNE_XXH64_WAVES = 15
-TUNE_XXH64_GLDS = 22
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -536,191 +536,6 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
     }
 }
 
-// Direct-to-LDS form of k_xxh64_lds (PCS_TUNE_XXH64_GLDS = D): each 256-byte
-// segment is fetched by four global_load_lds_dwordx4 wave-instructions straight
-// into a D-deep LDS ring, so the D - 1 segments in flight ahead of the one
-// being hashed cost no VGPRs (the register-staged kernel holds them in 16
-// VGPRs per segment and lost at depth 3-4: profiles/r02/x64_depth3_lab.txt).
-// An LDS-DMA instruction writes lane L's 16 bytes at base + 16 L, so the
-// bank swizzle of k_xxh64_lds moves to the SOURCE address (cdna_hip_
-// programming.md rule 21): lane t of row r in instruction ii fetches chunk
-// (t - 4 ii) & 15 of page 4 ii + r, which lands in slot t, exactly where the
-// register-staged kernel stores chunk (slot - 4 ii) & 15; the quad reads are
-// unchanged.  A lane with no byte to fetch is masked off (no traffic: config
-// 3's short pages would otherwise fetch padding), and an instruction no lane
-// of the wave needs is not issued; each segment's issued-instruction count is
-// wave-uniform (a ballot), so `s_waitcnt vmcnt(<instructions issued after
-// segment c>)` retires precisely the segment about to be hashed.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 63, "vmcnt field");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// s_waitcnt takes an immediate: dispatch a wave-uniform count 0..12
-__device__ __forceinline__ void wait_vmcnt_dyn(uint32_t n) {
-    switch (n) {
-        case 0: wait_vmcnt<0>(); break;
-        case 1: wait_vmcnt<1>(); break;
-        case 2: wait_vmcnt<2>(); break;
-        case 3: wait_vmcnt<3>(); break;
-        case 4: wait_vmcnt<4>(); break;
-        case 5: wait_vmcnt<5>(); break;
-        case 6: wait_vmcnt<6>(); break;
-        case 7: wait_vmcnt<7>(); break;
-        case 8: wait_vmcnt<8>(); break;
-        case 9: wait_vmcnt<9>(); break;
-        case 10: wait_vmcnt<10>(); break;
-        case 11: wait_vmcnt<11>(); break;
-        default: wait_vmcnt<12>(); break;
-    }
-}
-
-template <int MODE, bool NT, int ADDR, int D, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_xxh64_glds(const uint8_t* __restrict__ base,
-                                                        const uint64_t* __restrict__ off,
-                                                        const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
-                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                        unsigned long long* first_bad) {
-    static_assert(D >= 2 && D <= 4, "ring depth");
-    __shared__ __attribute__((aligned(16))) u32x4 lds[WPB][D][16][16];  // [wave][ring][page slot][16 B slot]
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int r = lane >> 4, t = lane & 15;        // loader role
-    const int i = (lane >> 2) & 3, q = lane & 3;   // hasher role: page 4i + r, quad lane q
-    const int a = q == 2 ? 3 : q == 3 ? 2 : q;
-    constexpr uint64_t kTile = 16 * WPB;
-    const uint64_t ntiles = (n + kTile - 1) / kTile;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t T = (remap ? xcd_tile(t0, ntiles) : t0) * kTile;
-        auto page_at = [&](int j) -> uint64_t { return T + wv * 16 + j; };
-        const uint8_t* lp[4];
-        uint32_t lP[4];
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-            const uint64_t pg = page_at(4 * ii + r);
-            uint32_t P = 0;
-            const uint8_t* p = nullptr;
-            if (pg < n) {
-                if (ADDR == kAddrDesc) {
-                    const uint64_t o = off[pg];
-                    const uint32_t L = len[pg];
-                    if (xxh64_lines_ok(o, L)) { P = L; p = base + o; }
-                } else if (ADDR == kAddrList) {
-                    P = Pfixed;
-                    p = reinterpret_cast<const uint8_t*>(off[pg]);
-                } else {
-                    P = Pfixed;
-                    p = base + pg * (uint64_t)Pfixed;
-                }
-            }
-            lp[ii] = p;
-            lP[ii] = P;
-        }
-        const uint64_t hp = page_at(4 * i + r);
-        uint32_t Ph = 0;
-        const uint8_t* hptr = nullptr;
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-            if (ii == i) { Ph = lP[ii]; hptr = lp[ii]; }
-        uint32_t segs;
-        {
-            uint32_t m = 0;
-#pragma unroll
-            for (int ii = 0; ii < 4; ++ii) m = max(m, lP[ii]);
-            m = max(m, (uint32_t)__shfl_xor((int)m, 16));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 32));
-            segs = __builtin_amdgcn_readfirstlane((m + 255) / 256);  // wave-uniform: scalar branches
-        }
-        // lane source per instruction ii: chunk (t - 4 ii) & 15 of its row's
-        // page; returns the instructions issued (wave-uniform)
-        auto issue = [&](uint32_t c) -> uint32_t {
-            uint32_t cnt = 0;
-#pragma unroll
-            for (int ii = 0; ii < 4; ++ii) {
-                const uint32_t at = 256 * c + 16 * ((t - 4 * ii) & 15);
-                const bool need = at < lP[ii];
-                if (__builtin_amdgcn_ballot_w64(need) != 0) {
-                    ++cnt;
-                    if (need)
-                        __builtin_amdgcn_global_load_lds(lp[ii] + at,
-                                                         (__attribute__((address_space(3))) void*)&lds[wv][c % D][4 * ii][0],
-                                                         16, 0, NT ? 2 : 0);
-                }
-            }
-            return __builtin_amdgcn_readfirstlane(cnt);
-        };
-        uint32_t issued[D];  // instructions issued per in-flight segment (ring order)
-        const int K = (int)(Ph / 64);
-        uint64_t v = xxh64_init(a), stored = 0;
-        u32x4 last = {0, 0, 0, 0};
-        // the ring slot about to be refilled was read in the previous step:
-        // those ds_reads are complete once their values were consumed
-#pragma unroll
-        for (int c = 0; c < D; ++c) issued[c] = 0;
-#pragma unroll
-        for (int c = 0; c < D - 1; ++c)
-            if ((uint32_t)c < segs) issued[c] = issue(c);  // wave-uniform
-        for (uint32_t c = 0; c < segs; ++c) {
-            if (c + D - 1 < segs) {
-                const uint32_t cnt = issue(c + D - 1);
-#pragma unroll
-                for (int j = 0; j < D; ++j)
-                    if ((uint32_t)j == (c + D - 1) % D) issued[j] = cnt;
-            }
-            // retire segment c: the instructions of the segments after it stay in flight
-            uint32_t after = 0;
-#pragma unroll
-            for (int j = 1; j < D; ++j)
-                if (c + j < segs) {
-#pragma unroll
-                    for (int x = 0; x < D; ++x)
-                        if ((uint32_t)x == (c + j) % D) after += issued[x];
-                }
-            wait_vmcnt_dyn(__builtin_amdgcn_readfirstlane(after));  // scalar branch: one wait runs
-            __builtin_amdgcn_wave_barrier();
-            const u32x4(*seg)[16] = lds[wv][c % D];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int kk = 4 * (int)c + k;
-                if (kk < K) {
-                    const u32x4 e = seg[4 * i + r][(4 * k + q + 4 * i) & 15];
-                    if (kk == 0) stored = dpp64<quad_bcast(0)>(lo64(e));
-                    if (kk == 0 || kk == K - 1)
-                        xxh64_chunk<true>(v, e, q, q == 2 && kk == 0, q != 2 && kk == K - 1);
-                    else xxh64_chunk<false>(v, e, q, false, false);
-                    if (kk == K - 1) last = e;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (K > 0) {
-            const uint64_t v0 = dpp64<quad_bcast(0)>(v);
-            const uint64_t v1 = dpp64<quad_bcast(1)>(v);
-            const uint64_t v2 = dpp64<quad_bcast(3)>(v);
-            const uint64_t v3 = dpp64<quad_bcast(2)>(v);
-            uint64_t h = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
-            h = (h ^ xxh64_round(0, v0)) * kP64_1 + kP64_4;
-            h = (h ^ xxh64_round(0, v1)) * kP64_1 + kP64_4;
-            h = (h ^ xxh64_round(0, v2)) * kP64_1 + kP64_4;
-            h = (h ^ xxh64_round(0, v3)) * kP64_1 + kP64_4;
-            h += (uint64_t)(Ph - 8);
-            const uint64_t t0w = dpp64<quad_bcast(2)>(hi64(last));
-            const uint64_t t1w = dpp64<quad_bcast(3)>(lo64(last));
-            const uint64_t t2w = dpp64<quad_bcast(3)>(hi64(last));
-            h ^= xxh64_round(0, t0w);
-            h = rotl64(h, 27) * kP64_1 + kP64_4;
-            h ^= xxh64_round(0, t1w);
-            h = rotl64(h, 27) * kP64_1 + kP64_4;
-            h ^= xxh64_round(0, t2w);
-            h = rotl64(h, 27) * kP64_1 + kP64_4;
-            h = xxh64_avalanche(h);
-            if (q == 0) emit(MODE, hp, h, stored, const_cast<uint8_t*>(hptr), out, ok, first_bad);
-        }
-        // the next tile's prologue refills ring slots this tile's last steps read
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
 // Pages off the 64-byte-piece shape (P % 64 != 0 or 8-byte-aligned only): one
 // quad per page, lane a reading accumulator a's words (xxh64_page).  The quad
 // layout for line-shaped pages (each quad loading its own 64 B pieces, 80 % of
@@ -1550,7 +1365,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 23;
+constexpr int kTuneKeys = 22;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1561,8 +1376,8 @@ constexpr int kTuneKeys = 23;
 // 20 4 KiB-aligned descriptor steps (+-0.2 %, aligned_steps_lab.txt), 21 the
 // descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt).
 // Setting one fails.
-constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
-                                      true,  false, true,  false, true,  true,  true,  true,  true,  true,  false};
+constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false,
+                                      true,  false, true,  false, true,  false, true,  true,  true,  true,  true,  true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1575,8 +1390,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4,
                                           /*retired*/ 0, /*retired*/ 0, /*retired*/ 0, /*retired*/ 0,
                                           /*retired*/ 0,
-                                          /*retired*/ 0,
-                                          /*xxh64 LDS kernel: direct-to-LDS ring depth (2-4; 0 = register staged)*/ 0};
+                                          /*retired*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1616,25 +1430,6 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
     const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
     const int64_t wpb = g_tune[15].load(std::memory_order_relaxed);
-    const int64_t glds = g_tune[22].load(std::memory_order_relaxed);
-    if (glds >= 2 && glds <= 4) {
-        const unsigned g = (wpb == 1 || wpb == 2)
-                               ? (unsigned)std::min<uint64_t>((n + 16 * wpb - 1) / (16 * wpb), 0x7FFFFFFFull)
-                               : grid;
-#define LG(D, W) hipLaunchKernelGGL((k_xxh64_glds<MODE, NT, ADDR, D, W>), dim3(g), dim3(64 * W), 0, s, base, off, len, P, n, out, ok, fb)
-#define LGW(W)                 \
-    do {                       \
-        if (glds == 2) LG(2, W); \
-        else if (glds == 3) LG(3, W); \
-        else LG(4, W);         \
-    } while (0)
-        if (wpb == 1) LGW(1);
-        else if (wpb == 2) LGW(2);
-        else LGW(4);
-#undef LGW
-#undef LG
-        return;
-    }
     if (wpb == 1 || wpb == 2) {
         // one workgroup per 16 * wpb pages, every tile covered once
         const unsigned g = (unsigned)std::min<uint64_t>((n + 16 * wpb - 1) / (16 * wpb), 0x7FFFFFFFull);

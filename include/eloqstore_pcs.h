@@ -244,15 +244,13 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
  *                                     kernel (1, 2 or 4; 16 pages per wave)
- *   PCS_TUNE_XXH64_GLDS           [0] XXH64 LDS kernel: segments fetched by
- *                                     direct-to-LDS loads into a ring this deep
- *                                     (2-4); 0 = staged through registers
- * Keys 4, 5, 10, 12, 14 and 16-21 selected variants that measured slower or no
+ * Keys 4, 5, 10, 12, 14 and 16-22 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
  * tiles, plain result stores, 4 KiB-aligned descriptor steps, a 4-waves-
- * per-SIMD descriptor body); they were retired in round 2:
- * setting one fails and reading one returns -1. */
+ * per-SIMD descriptor body; round 3: an XXH64 direct-to-LDS segment ring);
+ * they were retired: setting one fails and reading one
+ * returns -1. */
 enum pcs_tune_key {
     PCS_TUNE_XXH3_BLOCKS_PER_CU = 1,
     PCS_TUNE_XXH64_BLOCKS_PER_CU = 2,
@@ -264,7 +262,6 @@ enum pcs_tune_key {
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_WAVES = 15,
-    PCS_TUNE_XXH64_GLDS = 22,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -29,15 +29,12 @@ VARIANTS = {
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "x64_one_wave": {pcs.TUNE_XXH64_WAVES: 1},
     "x64_two_waves_depth4": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 4},
-    "x64_glds2": {pcs.TUNE_XXH64_GLDS: 2},
-    "x64_glds3_one_wave": {pcs.TUNE_XXH64_GLDS: 3, pcs.TUNE_XXH64_WAVES: 1},
-    "x64_glds4_two_waves": {pcs.TUNE_XXH64_GLDS: 4, pcs.TUNE_XXH64_WAVES: 2},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = [k for k in range(1, 23) if pcs.get_tuning(k) >= 0]  # retired keys read -1
+    keys = [k for k in range(1, 22) if pcs.get_tuning(k) >= 0]  # retired keys read -1
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -157,7 +154,7 @@ def test_desc_mixed_with_leftovers(tuned, mode):
 
 def test_retired_tuning_keys_fail():
     """Keys of the variants retired in round 2 are refused, and read -1."""
-    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 23, 99):
+    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 22, 99):
         assert pcs.get_tuning(k) == -1
         with pytest.raises(pcs.PcsError):
             pcs.set_tuning(k, 1)
