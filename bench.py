@@ -503,19 +503,37 @@ def batch_latency(pool, pageable, w: Workload):
     return out
 
 
-def timed_launches(w: Workload, mode: str, steps: int, warmup: int) -> float:
+def timed_launches(w: Workload, mode: str, steps: int, warmup: int, rounds: int = 1) -> float:
     """Average launch time (s) of `steps` back-to-back steps, bracketed by two
-    HIP events on the launch stream (torch's current stream)."""
+    HIP events on the launch stream (torch's current stream).  With rounds >
+    1 the steps run as that many bracketed rounds and the median round's
+    per-step time is returned: one host-side stall inside a round (a 1.1 ms
+    gap between two launches was seen in a 50-step sweep entry's trace,
+    profiles/r03b_sweep.json config 7) then moves one round, not the entry.
+    The garbage collector is held off while launches are timed."""
+    import gc
+    import statistics
+
     for _ in range(warmup):
         w.step(mode)
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for _ in range(steps):
-        w.step(mode)
-    ev1.record()
-    torch.cuda.synchronize()
-    return ev0.elapsed_time(ev1) / 1e3 / steps
+    per = max(1, steps // max(1, rounds))
+    times = []
+    gc_on = gc.isenabled()
+    gc.disable()
+    try:
+        for _ in range(max(1, rounds)):
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(per):
+                w.step(mode)
+            ev1.record()
+            torch.cuda.synchronize()
+            times.append(ev0.elapsed_time(ev1) / 1e3 / per)
+    finally:
+        if gc_on:
+            gc.enable()
+    return statistics.median(times)
 
 
 # (entry key, BASELINE config, algo, mode): every BASELINE config and mode the
@@ -529,6 +547,7 @@ SWEEP = (
     ("config2_xxh3_validate", 2, 0, "validate"),
     ("config2_xxh3_stamp", 2, 0, "stamp"),
 )
+SWEEP_ROUNDS = 5  # a sweep entry's steps run as this many bracketed rounds; the median round counts
 PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits the kernel trace on it
 
 
@@ -571,7 +590,8 @@ def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale):
     torch.cuda.synchronize()
     time.sleep(PHASE_GAP_S)
     t_wall0 = time.perf_counter()
-    avg = timed_launches(w, mode, steps, warmup)
+    rounds = SWEEP_ROUNDS if steps >= 2 * SWEEP_ROUNDS else 1
+    avg = timed_launches(w, mode, steps, warmup, rounds)
     t_wall = time.perf_counter() - t_wall0
     time.sleep(PHASE_GAP_S)
     alg = w.algorithmic_bytes(mode)
@@ -586,6 +606,7 @@ def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale):
          "avg_launch_ms": round(avg * 1e3, 4), "GiBps": round(w.bytes / avg / GIB, 1),
          "achieved_GBps": round(alg / avg / 1e9, 1), "frac": round(alg / avg / 1e9 / HBM_PEAK_GBPS, 4),
          "algorithmic_bytes_per_launch": alg, "wall_s": round(t_wall, 3),
+         "timing": f"median of {rounds} rounds of {max(1, steps // rounds)} steps, each bracketed by HIP events",
          "traffic": traffic[0] if traffic else None, "traffic_source": traffic[1] if traffic else None,
          "parity": par, "corruption_drill": drill}
     return e
@@ -705,6 +726,8 @@ def main():
     # bracketed average includes the dependent-kernel boundary (~2 us), so it
     # is an upper bound on the kernel time rocprofv3 reports.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    import gc
+    gc.disable()  # no collector pause between two timed launches
     barrier(dist)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -714,6 +737,7 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    gc.enable()
     barrier(dist)
     elapsed = max_over_ranks(dist, t1 - t0)
     avg_launch = ev0.elapsed_time(ev1) / 1e3 / args.steps
