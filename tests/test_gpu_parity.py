@@ -779,3 +779,24 @@ def test_manifest_forms_vs_oracle(wide):
         assert pcs.manifest_checksum_host(host[:3 * MiB + 5].tobytes()) == oracle.manifest_checksum(host[:3 * MiB + 5])
     finally:
         pcs.set_tuning(pcs.TUNE_MANIFEST_WIDE, saved)
+
+
+@pytest.mark.parametrize("P,n", [(131072, 3), (1 << 20, 2), ((16 << 20) + 256, 1), ((4 << 20) + 4104, 2)])
+@pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
+def test_huge_pages(P, n, algo):
+    """Pages far above EloqStore's 64 KiB (whole objects hashed with the page
+    convention): one group per page walks 128 KiB - 16 MiB (the run-time-size
+    and any-size bodies, the XXH64 LDS kernel at P % 64 == 0, the stride
+    kernel at P % 64 != 0).  Digest, stamp, validate, and a flip of the last
+    byte (the XXH3 last stripe / XXH64 tail), against the oracle."""
+    buf = dev_pages(P, n, 0xB16 + P, 3)
+    want = oracle.pages_digest(buf.cpu().numpy(), P, algo)
+    assert np.array_equal(u64(pcs.pages_digest(buf, P, n, algo)), want)
+    pcs.pages_stamp(buf, P, n, algo)
+    host = buf.cpu().numpy().reshape(n, P)
+    assert np.array_equal(host[:, :8].copy().view(np.uint64).ravel(), want)
+    ok, fb = pcs.pages_validate(buf, P, n, algo)
+    assert ok.cpu().numpy().all() and int(u64(fb)[0]) == (1 << 64) - 1
+    pcs.flip_byte(buf, P, n, every=n, byte_offset=P - 1)
+    ok, fb = pcs.pages_validate(buf, P, n, algo)
+    assert list(ok.cpu().numpy()) == [0] + [1] * (n - 1) and int(u64(fb)[0]) == 0
