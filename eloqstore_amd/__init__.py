@@ -151,6 +151,7 @@ TUNE_XXH3_SPLIT_PAGES = 9
 TUNE_INLINE_LIST = 11
 TUNE_MANIFEST_WIDE = 13
 TUNE_XXH64_WAVES = 15
+TUNE_ZC_POLL = 23
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -1365,7 +1365,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 22;
+constexpr int kTuneKeys = 24;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1374,10 +1374,11 @@ constexpr int kTuneKeys = 22;
 // split_pipe_lab.txt), 18 plain result stores (+-0.2 %, result_store_lab.txt),
 // 19 descriptor pages as a slice stream (-5..-8 %, desc_slices_lab.txt),
 // 20 4 KiB-aligned descriptor steps (+-0.2 %, aligned_steps_lab.txt), 21 the
-// descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt).
-// Setting one fails.
-constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false,
-                                      true,  false, true,  false, true,  false, true,  true,  true,  true,  true,  true};
+// descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt);
+// round 3: 22 the XXH64 direct-to-LDS segment ring (config 3 -0.8..-34 %,
+// profiles/r03/x64_glds_ab_*.txt).  Setting one fails.
+constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
+                                      true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1390,7 +1391,9 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*xxh64 LDS kernel: waves per workgroup (1, 2; else 4)*/ 4,
                                           /*retired*/ 0, /*retired*/ 0, /*retired*/ 0, /*retired*/ 0,
                                           /*retired*/ 0,
-                                          /*retired*/ 0};
+                                          /*retired*/ 0,
+                                          /*retired (round 3: XXH64 direct-to-LDS ring)*/ 0,
+                                          /*zero-copy validate: completion from the verdicts themselves*/ 1};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;

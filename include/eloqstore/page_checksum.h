@@ -40,7 +40,7 @@ bool ValidateChecksum(std::string_view blob);
 enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 
 // Batch-size policy for the call sites.  A GPU batch pays
-// a fixed launch + completion cost before any byte is hashed (~21 µs for one
+// a fixed launch + completion cost before any byte is hashed (~14 µs for one
 // page) while the reference's CPU loop pays per page (~0.6 µs per cache-cold
 // 4 KiB page), so small batches stay on the reference's own per-page
 // ValidateChecksum / SetChecksum (page.cpp:18-31): the 6-page scan prefetch
@@ -48,9 +48,10 @@ enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 // tail of a write batch.  Defaults are the measured latency crossovers of one
 // call against one core running the reference loop over the same scattered
 // 4 KiB pool pages (integration_snippets --crossover):
-//   registered pool (RegisterPagePool, zero-copy): GPU faster from 48 pages;
+//   registered pool (RegisterPagePool, zero-copy): GPU faster from 32-48
+//   pages (two boxes; 40 pages = 160 KiB is the default);
 //   unregistered pages (gathered into staging):    GPU faster from 192 pages.
-inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(192) << 10;
+inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(160) << 10;
 inline constexpr size_t kGpuChecksumMinBatchBytesStaged = size_t(768) << 10;
 inline bool GpuChecksumPays(size_t n_pages, size_t page_size, size_t min_bytes = kGpuChecksumMinBatchBytes) {
     return n_pages * page_size >= min_bytes;

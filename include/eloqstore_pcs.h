@@ -244,6 +244,10 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
  *                                     kernel (1, 2 or 4; 16 pages per wave)
+ *   PCS_TUNE_ZC_POLL              [1] zero-copy validate batches (sync and
+ *                                     async): complete once every verdict has
+ *                                     landed in host memory (1) or on the
+ *                                     launch's completion signal (0)
  * Keys 4, 5, 10, 12, 14 and 16-22 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -262,6 +266,7 @@ enum pcs_tune_key {
     PCS_TUNE_INLINE_LIST = 11,
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_WAVES = 15,
+    PCS_TUNE_ZC_POLL = 23,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

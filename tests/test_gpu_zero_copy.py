@@ -200,3 +200,46 @@ def test_batch_skip_verify_and_failed_submit():
         with pytest.raises(pcs.PcsError):
             b.result()
         b.close()
+
+
+@pytest.mark.parametrize("poll", [1, 0])
+def test_zero_copy_validate_completion_forms(poll):
+    """PCS_TUNE_ZC_POLL: a zero-copy validate completes when every verdict
+    has landed in host memory (1, default) or on the launch's completion
+    signal (0).  Back-to-back sync calls and async batches, inline (<= 256
+    pages) and host-memory page lists, each call with a different corrupted
+    page, the pool rewritten between calls: every verdict and first-bad index
+    must match the oracle."""
+    P = 4096
+    saved = pcs.get_tuning(pcs.TUNE_ZC_POLL)
+    pcs.set_tuning(pcs.TUNE_ZC_POLL, poll)
+    try:
+        with pcs.PagePool(1024, P) as pool:
+            pool.pages[:] = oracle.fill_pages(P, 1024, 0x2CC).reshape(1024, P)
+            for i in range(1024):
+                pool.pages[i, :8] = np.frombuffer(oracle.pages_digest(pool.pages[i], P, 0).tobytes(), np.uint8)
+            rng = np.random.default_rng(poll)
+            b1, b2 = pcs.Batch(), pcs.Batch()
+            try:
+                for it in range(40):
+                    n = (6, 48, 128, 256, 700, 1024)[it % 6]
+                    idx = rng.permutation(1024)[:n]
+                    ptrs = pool.ptr(idx)
+                    j = int(rng.integers(n))
+                    pool.pages[idx[j], 10] ^= 0x20
+                    ok, fb = pcs.validate_ptrs(ptrs, P)
+                    assert fb == j and np.flatnonzero(ok == 0).tolist() == [j], (it, n)
+                    b = b1 if it % 2 else b2
+                    b.submit_ptrs(pcs.Batch.VALIDATE, ptrs, P)
+                    while not b.poll():
+                        pass
+                    okb, fbb = b.result()
+                    assert fbb == j and okb.count(0) == 1, (it, n)
+                    pool.pages[idx[j], 10] ^= 0x20  # restore before the next round
+                    ok, fb = pcs.validate_ptrs(ptrs, P)
+                    assert ok.all() and fb is None
+            finally:
+                b1.close()
+                b2.close()
+    finally:
+        pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
