@@ -188,6 +188,7 @@ hipError_t wait_verdicts(const uint8_t* h_ok, uint64_t n, hipStream_t s) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return hipSuccess;
         }
+        __builtin_ia32_pause();  // spin politely: the sibling hyperthread may be a shard thread
         if ((spin & 4095) == 4095) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {  // finished: every verdict must be there now
