@@ -77,6 +77,9 @@ _SIGS = {
     "pcs_set_tuning": [_i32, ctypes.c_int64],
     "pcs_get_tuning": [_i32],
     "pcs_counter": [_i32],
+    "pcs_service_start": [_i32, _u32],
+    "pcs_service_stop": [],
+    "pcs_service_running": [],
     "pcs_version": [],
     "pcs_last_error": [],
 }
@@ -156,6 +159,7 @@ TUNE_ZC_POLL = 23
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1
 COUNTER_GATHER_CHUNKS = 2
+COUNTER_SERVICE_BATCHES = 3
 
 
 def counter(which: int) -> int:

@@ -51,4 +51,26 @@ int64_t get_tuning(int key);
 // folded word per 64 KiB window into out[0 .. ceil(bytes / 65536)).
 hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s);
 
+// Pre-armed validate service (pcs_service_*): a mailbox in pinned host
+// memory, read by the waiting kernel through its device alias.  Line 0
+// carries a whole small request (seq = generation << 32 | count, page count,
+// page size and the first five page addresses), so the kernel's poll brings
+// it in with one PCIe read; the host writes `seq` last.  Verdicts are 32-bit
+// words stored system-scope.
+constexpr int kServiceMaxPages = 256;
+constexpr uint32_t kServicePending = 0xA5A5A5A5u;
+struct ServiceBox {
+    alignas(64) uint64_t seq;
+    uint64_t n;
+    uint64_t page_size;
+    uint64_t ptrs[kServiceMaxPages];  // device-visible page addresses
+    alignas(64) uint64_t stop;        // host: 1 ends every waiting kernel
+    alignas(64) uint32_t ok[kServiceMaxPages];
+};
+// Queue one service kernel of generation `gen`: it serves that generation's
+// requests until idle_ticks pass without one or, between requests, it has
+// lived life_ticks (both on the 100 MHz real-time clock), or stop is set.
+hipError_t run_service(ServiceBox* d_box, int workgroups, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                       hipStream_t s);
+
 }  // namespace pcs

@@ -68,6 +68,14 @@ void UnregisterPagePool(void* base) {
     if (int rc = pcs_host_unregister(base)) die("UnregisterPagePool", rc);
 }
 
+void StartChecksumService(int workgroups, uint32_t idle_us) {
+    if (int rc = pcs_service_start(workgroups, idle_us)) die("StartChecksumService", rc);
+}
+
+void StopChecksumService() {
+    if (int rc = pcs_service_stop()) die("StopChecksumService", rc);
+}
+
 ChecksumBatch::ChecksumBatch() {
     if (int rc = pcs_batch_create(&batch_)) die("ChecksumBatch", rc);
 }

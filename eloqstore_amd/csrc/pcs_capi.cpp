@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -155,7 +156,7 @@ struct ZcBufs {
     }
 };
 
-std::atomic<uint64_t> g_counters[3];
+std::atomic<uint64_t> g_counters[4];
 void count(int which) { g_counters[which].fetch_add(1, std::memory_order_relaxed); }
 
 int64_t zero_copy_policy() { return pcs::get_tuning(PCS_TUNE_ZERO_COPY); }
@@ -483,6 +484,142 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
     return rc;
 }
 
+// ---------------------------------------------------------------------------
+// pre-armed validate service (pcs_service_*)
+// ---------------------------------------------------------------------------
+// One service per process, on the device current at pcs_service_start; one
+// request in flight (callers serialise on the mutex).  Requests are served by
+// a resident kernel (pcs_kernels.hip k_service) that leaves after idle_us
+// without a request or, between requests, after 2 * idle_us of life.  The
+// host tracks both clocks from its side (conservatively: the kernel starts
+// after its launch call and restarts its idle clock before the host sees the
+// verdicts); while it is sure, by a margin of idle_us / 4, that the kernel is
+// still waiting, a request is one mailbox write and a spin on the verdicts.
+// Otherwise it starts the next generation (queued behind the old kernel,
+// which ignores the new requests and leaves within the margin).
+struct Service {
+    using clock = std::chrono::steady_clock;
+    std::mutex mu;
+    int device = -1;
+    int workgroups = 0;
+    uint32_t idle_us = 0;
+    hipStream_t stream = nullptr;
+    pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped
+    pcs::ServiceBox* d = nullptr;  // its device alias
+    uint32_t gen = 0;              // generation of the newest queued kernel
+    uint32_t count = 0;            // requests posted to it
+    bool live = false;             // it has been queued (it may have left since)
+    clock::time_point launched, answered;
+    bool exit_hook = false;
+};
+Service g_service;
+std::atomic<bool> g_service_on{false};
+
+int service_launch_locked(Service& sv) {
+    ++sv.gen;
+    sv.count = 0;
+    sv.live = true;
+    sv.launched = sv.answered = Service::clock::now();
+    return finish(pcs::run_service(sv.d, sv.workgroups, sv.gen, (uint64_t)sv.idle_us * 100,
+                                   (uint64_t)sv.idle_us * 200, sv.stream),
+                  "service kernel launch");
+}
+
+// Certainly still waiting: launched less than life - margin ago and last
+// answered less than idle - margin ago (host time bounds the kernel's clocks).
+bool service_waiting(const Service& sv, Service::clock::time_point now) {
+    const auto margin = std::chrono::microseconds(sv.idle_us / 4);
+    return sv.live && now - sv.launched < std::chrono::microseconds(2 * (uint64_t)sv.idle_us) - margin &&
+           now - sv.answered < std::chrono::microseconds(sv.idle_us) - margin;
+}
+
+void service_post(Service& sv) {
+    std::atomic_thread_fence(std::memory_order_release);
+    __atomic_store_n(&sv.h->seq, (uint64_t)sv.gen << 32 | ++sv.count, __ATOMIC_RELEASE);
+}
+
+int service_stop_locked(Service& sv) {
+    if (sv.device < 0) return PCS_OK;
+    g_service_on.store(false, std::memory_order_relaxed);
+    __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);  // every queued kernel leaves at its next poll
+    int cur = -1;
+    const bool other = hipGetDevice(&cur) == hipSuccess && cur != sv.device;
+    if (other) (void)hipSetDevice(sv.device);
+    const hipError_t e = hipStreamSynchronize(sv.stream);
+    (void)hipStreamDestroy(sv.stream);
+    (void)hipHostFree(sv.h);
+    if (other) (void)hipSetDevice(cur);
+    sv.stream = nullptr;
+    sv.h = sv.d = nullptr;
+    sv.device = -1;
+    sv.live = false;
+    return finish(e, "service stop");
+}
+
+// Process exit with the service on: end the queued kernels before the HIP
+// runtime tears down (handlers registered after the runtime's first use run
+// before its own destructors).
+void service_at_exit() {
+    std::lock_guard<std::mutex> lk(g_service.mu);
+    (void)service_stop_locked(g_service);
+}
+
+constexpr int kNotServed = 1;  // service_validate: not eligible, the caller takes the launch path
+
+// A host validate batch through the service: XXH3, registered 16-byte-aligned
+// pages with page_size % 256 == 0, 1..256 pages, on the service's device.
+int service_validate(const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok, uint64_t* first_bad) {
+    if (algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
+        return kNotServed;
+    Service& sv = g_service;
+    std::lock_guard<std::mutex> lk(sv.mu);
+    if (sv.device < 0) return kNotServed;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != sv.device) return kNotServed;
+    if (!g_regions.translate(pages, n, P, sv.h->ptrs)) return kNotServed;
+    sv.h->n = n;
+    sv.h->page_size = P;
+    for (uint64_t i = 0; i < n; ++i) sv.h->ok[i] = pcs::kServicePending;
+    if (!service_waiting(sv, Service::clock::now()))
+        if (int rc = service_launch_locked(sv)) return rc;
+    service_post(sv);
+    const volatile uint32_t* v = sv.h->ok;
+    uint64_t at = 0;
+    int relaunched = 0;
+    const auto t0 = Service::clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        while (at < n && v[at] != pcs::kServicePending) ++at;
+        if (at == n) break;
+        __builtin_ia32_pause();
+        if ((spin & 4095) != 4095) continue;
+        const hipError_t q = hipStreamQuery(sv.stream);
+        if (q == hipSuccess) {
+            // every queued kernel has left and this request is not fully
+            // answered (a workgroup reached its limit just before the post):
+            // a new generation serves it again (verdicts are idempotent)
+            while (at < n && v[at] != pcs::kServicePending) ++at;
+            if (at == n) break;
+            if (++relaunched > 2) return fail(PCS_ERR_HIP, "validate service: request not answered");
+            if (int rc = service_launch_locked(sv)) return rc;
+            service_post(sv);
+        } else if (q != hipErrorNotReady) {
+            return hip_fail(q, "service stream");
+        }
+        if (Service::clock::now() - t0 > std::chrono::seconds(5))
+            return fail(PCS_ERR_HIP, "validate service: no answer within 5 s");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    sv.answered = Service::clock::now();
+    uint64_t bad = UINT64_MAX;
+    for (uint64_t i = 0; i < n; ++i) {
+        ok[i] = (uint8_t)sv.h->ok[i];
+        if (!ok[i] && bad == UINT64_MAX) bad = i;
+    }
+    if (first_bad) *first_bad = bad;
+    count(PCS_COUNTER_SERVICE_BATCHES);
+    return PCS_OK;
+}
+
 // Device copy of one host buffer + a result word, for the manifest host API.
 int manifest_host(const void* content, uint64_t len, uint64_t* out) {
     if (int rc = require_device()) return rc;
@@ -642,7 +779,58 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
         if (first_bad) *first_bad = UINT64_MAX;
         return PCS_OK;
     }
+    if (g_service_on.load(std::memory_order_relaxed)) {
+        if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
+        const int r = service_validate(pages, page_size, n_pages, algo, ok, first_bad);
+        if (r != kNotServed) return r;
+    }
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
+}
+
+int pcs_service_start(int workgroups, uint32_t idle_us) {
+    if (workgroups < 1 || workgroups > 256) return fail(PCS_ERR_INVALID, "workgroups must be in [1, 256]");
+    if (idle_us && (idle_us < 200 || idle_us > 1000000))
+        return fail(PCS_ERR_INVALID, "idle_us must be 0 (1000) or in [200, 1000000]");
+    if (int rc = require_device()) return rc;
+    Service& sv = g_service;
+    std::lock_guard<std::mutex> lk(sv.mu);
+    if (sv.device >= 0) return fail(PCS_ERR_INVALID, "the validate service is already running");
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "service start");
+    if (hipHostMalloc(reinterpret_cast<void**>(&sv.h), sizeof(pcs::ServiceBox),
+                      hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        (void)hipStreamDestroy(sv.stream);
+        sv.stream = nullptr;
+        return fail(PCS_ERR_NOMEM, "service mailbox allocation failed");
+    }
+    std::memset(static_cast<void*>(sv.h), 0, sizeof(pcs::ServiceBox));
+    sv.d = dev_alias(sv.h);
+    sv.device = dev;
+    sv.workgroups = workgroups;
+    sv.idle_us = idle_us ? idle_us : 1000;
+    sv.live = false;
+    if (!sv.d) {
+        (void)service_stop_locked(sv);
+        return fail(PCS_ERR_HIP, "service mailbox has no device alias");
+    }
+    if (!sv.exit_hook) {
+        std::atexit(service_at_exit);
+        sv.exit_hook = true;
+    }
+    g_service_on.store(true, std::memory_order_relaxed);
+    return PCS_OK;
+}
+
+int pcs_service_stop(void) {
+    std::lock_guard<std::mutex> lk(g_service.mu);
+    return service_stop_locked(g_service);
+}
+
+int pcs_service_running(void) {
+    std::lock_guard<std::mutex> lk(g_service.mu);
+    return g_service.device >= 0 ? 1 : 0;
 }
 
 int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_pages, int algo) {
@@ -933,7 +1121,7 @@ int pcs_set_tuning(int key, int64_t value) {
 int64_t pcs_get_tuning(int key) { return pcs::get_tuning(key); }
 
 uint64_t pcs_counter(int which) {
-    return (which < 0 || which > 2) ? 0 : g_counters[which].load(std::memory_order_relaxed);
+    return (which < 0 || which > 3) ? 0 : g_counters[which].load(std::memory_order_relaxed);
 }
 
 int pcs_gen_pages_dev(void* d_pages, uint64_t page_size, uint64_t n_pages, uint64_t seed, uint64_t first_page_index,

@@ -1783,6 +1783,88 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Pre-armed validate service (pcs_service_*, SURVEY.md §8f-1: small
+// ReadPages batches).  A launch per host batch costs ~14 µs before its first
+// page is read; here a kernel stays resident between requests, polling the
+// request line in pinned host memory, so a request finds it waiting: ~7.5 µs
+// for one page (tools/lab/service_lab.hip, profiles/r03/service_lab.txt).
+// The kernel leaves after idle_ticks without a request and, between
+// requests, once it has lived life_ticks, so a device-synchronising call
+// elsewhere in the process waits at most that long (a grid that never leaves
+// blocks such calls for as long as requests keep coming); the
+// host starts the next generation of it when it can no longer be sure one is
+// waiting.  A kernel serves only requests of its own generation (the high 32
+// bits of seq), so a late kernel of an earlier generation never serves a
+// request twice.  8 lanes of each workgroup poll line 0 whole (x86 serves a
+// 64-byte read of one host line as one snapshot, and the host writes seq
+// last); on a new seq the workgroup runs a system-scope acquire (the pages
+// and the rest of the list are read fresh from host memory), hashes pages
+// blockIdx.x * 16 + group, stride gridDim.x * 16 (the run-time-size XXH3
+// body: registered 16-byte-aligned pages, page_size % 256 == 0) and stores
+// each verdict word system-scope, which reaches host memory without a
+// release fence.
+__global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, uint64_t idle_ticks,
+                                                 uint64_t life_ticks) {
+    __shared__ uint64_t s_line[8];
+    __shared__ int s_go;
+    const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
+    const uint64_t born = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_last = born;
+    uint64_t last = gen << 32;  // this generation's requests carry gen << 32 | count, count from 1
+    for (;;) {
+        if (threadIdx.x < 8) {
+            const uint64_t* line = &box->seq;
+            uint64_t w = 0;
+            int go = 0;
+            for (;;) {
+                w = __hip_atomic_load(line + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t w0 = __shfl(w, 0, 8);
+                if (w0 != last && (w0 >> 32) == gen) {
+                    go = 1;
+                    break;
+                }
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (__hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    now - t_last > idle_ticks || now - born > life_ticks)
+                    break;
+            }
+            s_line[threadIdx.x] = w;
+            if (threadIdx.x == 0) s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;  // uniform per workgroup: idle, lifetime or stop
+        last = s_line[0];
+        const uint64_t n = s_line[1];
+        const uint32_t P = (uint32_t)s_line[2];
+        uint64_t head[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) head[k] = s_line[3 + k];
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        for (uint64_t pg = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 4); pg < n; pg += (uint64_t)gridDim.x * 16) {
+            uint64_t a = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                if (pg == (uint64_t)k) a = head[k];
+            if (pg >= 5) a = __hip_atomic_load(&box->ptrs[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            uint64_t stored = 0;
+            const uint64_t h = xxh3_page_rt4<false>(reinterpret_cast<const uint8_t*>(a), P, L, stored);
+            if (L.g == 0)
+                __hip_atomic_store(&box->ok[pg], h == stored ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();  // every lane has read s_line and s_go before the next poll rewrites them
+        t_last = __builtin_amdgcn_s_memrealtime();  // the idle clock starts after this workgroup's verdicts
+    }
+}
+
+hipError_t run_service(ServiceBox* d_box, int workgroups, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                       hipStream_t s) {
+    if (workgroups < 1 || workgroups > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_service, dim3((unsigned)workgroups), dim3(kBlock), 0, s, d_box, (uint64_t)gen, idle_ticks,
+                       life_ticks);
+    return hipGetLastError();
+}
+
 hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s) {
     if (bytes < 16) return hipSuccess;
     const uint64_t nwin = (bytes + kStreamWin - 1) / kStreamWin;

@@ -192,6 +192,25 @@ int pcs_batch_wait(pcs_batch *b);   /* blocks until done; PCS_OK or error */
 int pcs_batch_result(pcs_batch *b, uint8_t *ok, uint64_t *digests, uint64_t *first_bad);
 int pcs_batch_destroy(pcs_batch *b);
 
+/* ---- pre-armed validate service (small read batches, opt-in) --------------
+ * A launch per host batch costs ~14 µs before its first page is read.  While
+ * the service is on, pcs_pages_validate_host(_ex) (and so
+ * eloqstore::ValidateChecksums) serves eligible batches through a resident
+ * kernel of `workgroups` workgroups that polls a request line in pinned host
+ * memory between requests.  Eligible: XXH3, 1-256 pages, all in registered
+ * regions, 16-byte aligned, page_size % 256 == 0, on the device that started
+ * the service; everything else takes the launch path.  One request is in
+ * flight at a time (calls from several threads serialise).  The kernel leaves
+ * after idle_us (0 = 1000; else 200 .. 1000000) without a request and, between
+ * requests, after 2 * idle_us of life, and the next request starts a new one:
+ * it holds its CUs, and delays any device-synchronising HIP call of the
+ * process, by at most 2 * idle_us.  Results are identical to the launch
+ * path's.  PCS_ERR_INVALID for workgroups outside [1, 256] or
+ * an idle_us out of range, or when the service is already running. */
+int pcs_service_start(int workgroups, uint32_t idle_us);
+int pcs_service_stop(void);
+int pcs_service_running(void); /* 1 while the service is on, 0 otherwise */
+
 /* ---- manifest record checksum (next row: SURVEY.md §8f-3) -----------------
  * ManifestBuilder::CalcChecksum (src/storage/root_meta.cpp:150-174): XXH3-64
  * of each <= 1 MiB chunk of the content, folded as agg = rotl(agg, 1) ^ h;
@@ -277,6 +296,7 @@ enum pcs_counter {
     PCS_COUNTER_ZERO_COPY_LAUNCHES = 0, /* registered pages hashed in place */
     PCS_COUNTER_DIRECT_DMA_CHUNKS = 1,  /* contiguous pinned runs DMA'd as is */
     PCS_COUNTER_GATHER_CHUNKS = 2,      /* pages gathered into pinned staging */
+    PCS_COUNTER_SERVICE_BATCHES = 3,    /* validate batches served by the pre-armed service */
 };
 uint64_t pcs_counter(int which); /* 0 for an unknown counter */
 

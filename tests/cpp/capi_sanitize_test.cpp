@@ -92,6 +92,11 @@ static void no_device() {
     CHECK(pcs_host_register(page.data(), page.size()) == PCS_ERR_NO_DEVICE);
     pcs_batch* b = reinterpret_cast<pcs_batch*>(0x1);
     CHECK(pcs_batch_create(&b) == PCS_ERR_NO_DEVICE && b == nullptr);
+    CHECK(pcs_service_start(4, 0) == PCS_ERR_NO_DEVICE);
+    CHECK(pcs_service_start(0, 0) == PCS_ERR_INVALID);
+    CHECK(pcs_service_start(4, 2000000) == PCS_ERR_INVALID);
+    CHECK(pcs_service_start(4, 100) == PCS_ERR_INVALID);
+    CHECK(pcs_service_running() == 0 && pcs_service_stop() == PCS_OK);
 }
 
 static void arguments() {

@@ -1,0 +1,196 @@
+"""Pre-armed validate service (pcs_service_*): while it is on, host validate
+batches of up to 256 registered pages are served by a resident kernel polling
+a request line in pinned memory (small ReadPages batches);
+it leaves after idle_us without a request or 2 * idle_us of life and the next
+request starts a new generation.  Every verdict and first-bad index is checked
+against the CPU oracle; the path counters prove which path served each batch.
+Batches the service does not take (more than 256 pages, pages outside
+registered memory, XXH64, page sizes off the 256-byte grid) come back right
+through the launch path, and the resident kernel holds up a
+device-synchronising call for no longer than its limits."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import eloqstore_amd as pcs
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+SVC = pcs.COUNTER_SERVICE_BATCHES
+ZC = pcs.COUNTER_ZERO_COPY_LAUNCHES
+
+
+@pytest.fixture
+def service():
+    assert pcs.lib().pcs_service_running() == 0
+    pcs._call("pcs_service_start", 4, 1000)
+    try:
+        yield
+    finally:
+        pcs._call("pcs_service_stop")
+    assert pcs.lib().pcs_service_running() == 0
+
+
+def stamped_pool(n, P, seed):
+    pool = pcs.PagePool(n, P)
+    pool.pages[:] = oracle.fill_pages(P, n, seed).reshape(n, P)
+    pcs.stamp_ptrs(pool.ptr(np.arange(n)), P)
+    return pool
+
+
+def counters():
+    return pcs.counter(SVC), pcs.counter(ZC)
+
+
+@pytest.mark.parametrize("P", [4096, 16384, 1280])
+def test_service_serves_small_batches(service, P):
+    n_pool = 1024 if P <= 4096 else 256
+    with stamped_pool(n_pool, P, 0x5E1 + P) as pool:
+        rng = np.random.default_rng(P)
+        for n in (1, 5, 6, 7, 16, 100, 256):
+            idx = rng.permutation(n_pool)[:n]
+            ptrs = pool.ptr(idx)
+            s0, z0 = counters()
+            ok, fb = pcs.validate_ptrs(ptrs, P)
+            assert ok.all() and fb is None
+            assert counters() == (s0 + 1, z0), n
+            for j in sorted({0, n // 2, n - 1}):
+                pool.pages[idx[j], P - 1] ^= 0x01  # the last stripe
+                ok, fb = pcs.validate_ptrs(ptrs, P)
+                hdr = pool.pages[idx, :8].copy().view(np.uint64).ravel()
+                want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0) == hdr
+                assert np.array_equal(ok.astype(bool), want) and fb == j, (n, j)
+                pool.pages[idx[j], P - 1] ^= 0x01
+
+
+def test_service_idle_gaps(service):
+    """Requests spaced wider than the idle limit find their kernel gone and
+    start the next generation; gaps near the limit may find the old one
+    leaving; results stay exact."""
+    P = 4096
+    with stamped_pool(64, P, 0x5E2) as pool:
+        for gap in (0.0, 0.002, 0.0, 0.01, 0.0005, 0.0007, 0.0008, 0.0009, 0.001, 0.0011, 0.0, 0.0):
+            time.sleep(gap)
+            pool.pages[7, 10] ^= 0x01
+            s0, _ = counters()
+            ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(16)), P)
+            assert fb == 7 and ok.sum() == 15 and pcs.counter(SVC) == s0 + 1
+            pool.pages[7, 10] ^= 0x01
+
+
+def test_service_declines_what_it_cannot_serve(service):
+    P = 4096
+    with stamped_pool(512, P, 0x5E9) as pool:
+        idx = np.arange(300)  # more than 256 pages
+        pool.pages[idx[257], 10] ^= 0xFF
+        s0, z0 = counters()
+        ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+        assert fb == 257 and ok.sum() == 299
+        assert counters() == (s0, z0 + 1)
+        pool.pages[idx[257], 10] ^= 0xFF
+        pcs.stamp_ptrs(pool.ptr(np.arange(16)), P, pcs.XXH64)
+        s0, _ = counters()
+        ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(16)), P, pcs.XXH64)
+        assert ok.all() and fb is None and pcs.counter(SVC) == s0
+    pages = [bytearray(oracle.fill_pages(P, 1, 0x5EA + i).tobytes()) for i in range(8)]
+    for pg in pages:
+        pcs.set_checksum(pg)
+    s0, _ = counters()
+    ok, fb = pcs.validate_checksums(pages, P)
+    assert ok == [1] * 8 and fb is None and pcs.counter(SVC) == s0
+
+
+def test_service_under_threads(service):
+    """Four threads validating at once: requests serialise on the service and
+    each thread gets its own batch's verdicts."""
+    P = 4096
+    with stamped_pool(1024, P, 0x5EB) as pool:
+        errors = []
+
+        def worker(t):
+            rng = np.random.default_rng(100 + t)
+            try:
+                for _ in range(60):
+                    n = int(rng.integers(1, 64))
+                    idx = rng.permutation(1024)[:n]
+                    ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                    if not (ok.all() and fb is None):
+                        errors.append((t, n, fb))
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        s0, _ = counters()
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors
+        assert pcs.counter(SVC) - s0 == 240
+
+
+def test_resident_kernel_does_not_hold_up_device_sync(service):
+    """Right after a request the kernel is still resident and polling; a
+    device-synchronising call elsewhere (unregistering another pool chunk)
+    comes back once it leaves (1 ms idle), also while another thread keeps
+    requests coming (2 ms of life at most)."""
+    P = 4096
+    with stamped_pool(64, P, 0x5EE) as pool:
+        other = pcs.PagePool(16, P)
+        ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(8)), P)
+        assert ok.all()
+        t0 = time.perf_counter()
+        other.close()  # hipHostUnregister
+        assert time.perf_counter() - t0 < 0.5
+        ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(8)), P)  # still served afterwards
+        assert ok.all() and fb is None
+
+        stop = threading.Event()
+        served = []
+
+        def traffic():
+            k = 0
+            while not stop.is_set():
+                ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(8)), P)
+                k += int(ok.all() and fb is None)
+            served.append(k)
+
+        th = threading.Thread(target=traffic)
+        th.start()
+        try:
+            time.sleep(0.05)
+            for _ in range(3):
+                other = pcs.PagePool(16, P)
+                t0 = time.perf_counter()
+                other.close()
+                assert time.perf_counter() - t0 < 0.5
+        finally:
+            stop.set()
+            th.join()
+        assert served and served[0] > 10
+
+
+def test_service_lifecycle():
+    P = 4096
+    for bad in ((0, 0), (257, 0), (4, 100), (4, 2000000)):
+        with pytest.raises(pcs.PcsError):
+            pcs._call("pcs_service_start", *bad)
+    with stamped_pool(64, P, 0x5EC) as pool:
+        ptrs = pool.ptr(np.arange(8))
+        for _round in range(2):  # start, serve, stop, and again
+            pcs._call("pcs_service_start", 2, 0)
+            try:
+                with pytest.raises(pcs.PcsError):
+                    pcs._call("pcs_service_start", 2, 0)  # already running
+                s0, _ = counters()
+                ok, fb = pcs.validate_ptrs(ptrs, P)
+                assert ok.all() and fb is None and pcs.counter(SVC) == s0 + 1
+            finally:
+                pcs._call("pcs_service_stop")
+            s0, z0 = counters()
+            ok, fb = pcs.validate_ptrs(ptrs, P)  # after stop: the launch path
+            assert ok.all() and counters() == (s0, z0 + 1)
+        pcs._call("pcs_service_stop")  # stopping a stopped service is fine
