@@ -426,6 +426,22 @@ def digest_ptrs(ptrs, page_size: int, algo: int = XXH3_64) -> np.ndarray:
     return out[: len(ptrs)]
 
 
+class ValidateService:
+    """pcs_service_start / pcs_service_stop as a context manager: while it is
+    open, validate_ptrs / validate_checksums batches of up to 256 registered
+    XXH3 pages go to a resident kernel instead of a launch each."""
+
+    def __init__(self, workgroups: int = 4, idle_us: int = 1000):
+        self.workgroups, self.idle_us = workgroups, idle_us
+
+    def __enter__(self):
+        _call("pcs_service_start", self.workgroups, self.idle_us)
+        return self
+
+    def __exit__(self, *exc):
+        _call("pcs_service_stop")
+
+
 class PagePool:
     """A page-aligned host region of n_pages x page_size, like one chunk of
     EloqStore's PagesPool (page.cpp:95-120), registered for zero-copy batches.

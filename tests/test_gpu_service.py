@@ -26,11 +26,9 @@ ZC = pcs.COUNTER_ZERO_COPY_LAUNCHES
 @pytest.fixture
 def service():
     assert pcs.lib().pcs_service_running() == 0
-    pcs._call("pcs_service_start", 4, 1000)
-    try:
+    with pcs.ValidateService(4, 1000):
+        assert pcs.lib().pcs_service_running() == 1
         yield
-    finally:
-        pcs._call("pcs_service_stop")
     assert pcs.lib().pcs_service_running() == 0
 
 
