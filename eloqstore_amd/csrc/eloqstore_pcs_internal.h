@@ -59,10 +59,11 @@ hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hi
 // words stored system-scope.
 constexpr int kServiceMaxPages = 256;
 constexpr uint32_t kServicePending = 0xA5A5A5A5u;
+constexpr uint64_t kServiceStamp = 1ull << 32;  // in the page-size word: a stamp request
 struct ServiceBox {
     alignas(64) uint64_t seq;
     uint64_t n;
-    uint64_t page_size;
+    uint64_t page_size;               // | kServiceStamp for a stamp request
     uint64_t ptrs[kServiceMaxPages];  // device-visible page addresses
     alignas(64) uint64_t stop;        // host: 1 ends every waiting kernel
     alignas(64) uint32_t ok[kServiceMaxPages];

@@ -564,11 +564,12 @@ void service_at_exit() {
     (void)service_stop_locked(g_service);
 }
 
-constexpr int kNotServed = 1;  // service_validate: not eligible, the caller takes the launch path
+constexpr int kNotServed = 1;  // service_run: not eligible, the caller takes the launch path
 
-// A host validate batch through the service: XXH3, registered 16-byte-aligned
-// pages with page_size % 256 == 0, 1..256 pages, on the service's device.
-int service_validate(const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok, uint64_t* first_bad) {
+// A host validate (ok != null) or stamp (ok == null) batch through the
+// service: XXH3, registered 16-byte-aligned pages with page_size % 256 == 0,
+// 1..256 pages, on the service's device.
+int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok, uint64_t* first_bad) {
     if (algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
         return kNotServed;
     Service& sv = g_service;
@@ -578,7 +579,7 @@ int service_validate(const void* const* pages, uint64_t P, uint64_t n, int algo,
     if (hipGetDevice(&dev) != hipSuccess || dev != sv.device) return kNotServed;
     if (!g_regions.translate(pages, n, P, sv.h->ptrs)) return kNotServed;
     sv.h->n = n;
-    sv.h->page_size = P;
+    sv.h->page_size = P | (ok ? 0 : pcs::kServiceStamp);
     for (uint64_t i = 0; i < n; ++i) sv.h->ok[i] = pcs::kServicePending;
     if (!service_waiting(sv, Service::clock::now()))
         if (int rc = service_launch_locked(sv)) return rc;
@@ -610,12 +611,17 @@ int service_validate(const void* const* pages, uint64_t P, uint64_t n, int algo,
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     sv.answered = Service::clock::now();
-    uint64_t bad = UINT64_MAX;
-    for (uint64_t i = 0; i < n; ++i) {
-        ok[i] = (uint8_t)sv.h->ok[i];
-        if (!ok[i] && bad == UINT64_MAX) bad = i;
+    if (ok) {
+        uint64_t bad = UINT64_MAX;
+        for (uint64_t i = 0; i < n; ++i) {
+            ok[i] = (uint8_t)sv.h->ok[i];
+            if (!ok[i] && bad == UINT64_MAX) bad = i;
+        }
+        if (first_bad) *first_bad = bad;
+    } else {
+        for (uint64_t i = 0; i < n; ++i)
+            if (sv.h->ok[i] != 1u) return fail(PCS_ERR_HIP, "validate service: stamp not confirmed");
     }
-    if (first_bad) *first_bad = bad;
     count(PCS_COUNTER_SERVICE_BATCHES);
     return PCS_OK;
 }
@@ -781,7 +787,7 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
     }
     if (g_service_on.load(std::memory_order_relaxed)) {
         if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
-        const int r = service_validate(pages, page_size, n_pages, algo, ok, first_bad);
+        const int r = service_run(pages, page_size, n_pages, algo, ok, first_bad);
         if (r != kNotServed) return r;
     }
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
@@ -834,6 +840,12 @@ int pcs_service_running(void) {
 }
 
 int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_pages, int algo) {
+    if (g_service_on.load(std::memory_order_relaxed)) {
+        const void* const* cp = const_cast<const void* const*>(pages);
+        if (int rc = check_host_batch_args(cp, page_size, n_pages, algo)) return rc;
+        const int r = service_run(cp, page_size, n_pages, algo, nullptr, nullptr);
+        if (r != kNotServed) return r;
+    }
     return host_batch(2, const_cast<const void* const*>(pages), page_size, n_pages, algo, nullptr, nullptr, nullptr);
 }
 

@@ -1803,7 +1803,9 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // blockIdx.x * 16 + group, stride gridDim.x * 16 (the run-time-size XXH3
 // body: registered 16-byte-aligned pages, page_size % 256 == 0) and stores
 // each verdict word system-scope, which reaches host memory without a
-// release fence.
+// release fence.  A stamp request (high half of the page-size word) stores
+// the digest into the page header instead and then a done word, released
+// after it.
 __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, uint64_t idle_ticks,
                                                  uint64_t life_ticks) {
     __shared__ uint64_t s_line[8];
@@ -1837,6 +1839,7 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, 
         last = s_line[0];
         const uint64_t n = s_line[1];
         const uint32_t P = (uint32_t)s_line[2];
+        const bool stamp = (s_line[2] >> 32) != 0;  // kServiceStamp: write the digest into the header
         uint64_t head[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) head[k] = s_line[3 + k];
@@ -1849,8 +1852,17 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, 
             if (pg >= 5) a = __hip_atomic_load(&box->ptrs[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             uint64_t stored = 0;
             const uint64_t h = xxh3_page_rt4<false>(reinterpret_cast<const uint8_t*>(a), P, L, stored);
-            if (L.g == 0)
-                __hip_atomic_store(&box->ok[pg], h == stored ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (L.g == 0) {
+                if (stamp) {
+                    // the header, then the done word released after it: the
+                    // host sees the word only once the header has landed
+                    __hip_atomic_store(reinterpret_cast<uint64_t*>(a), h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&box->ok[pg], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                } else {
+                    __hip_atomic_store(&box->ok[pg], h == stored ? 1u : 0u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         }
         __syncthreads();  // every lane has read s_line and s_go before the next poll rewrites them
         t_last = __builtin_amdgcn_s_memrealtime();  // the idle clock starts after this workgroup's verdicts

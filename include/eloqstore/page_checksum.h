@@ -89,17 +89,18 @@ void RegisterPagePool(void* base, size_t bytes);
 void UnregisterPagePool(void* base);
 
 // Pre-armed validate service (pcs_service_start, opt-in): while it is on,
-// ValidateChecksums serves batches of up to 256 registered pages through a
-// resident kernel polling a request line, instead of a launch per batch, and
-// the GPU pays from kGpuChecksumMinBatchBytesService on (4 KiB pool pages:
-// 1 page 8.2-8.9 µs instead of 13.8-15.1; faster than the reference loop from
-// 20-24 pages on two boxes, integration_snippets --crossover).  The kernel
-// holds `workgroups` CUs (16 serves 128-256 pages 10-15 % faster than 4) and
-// leaves after idle_us without a request or 2 * idle_us of life; the next
-// request starts a new one.
+// ValidateChecksums and SetChecksums serve batches of up to 256 registered
+// pages through a resident kernel polling a request line, instead of a launch
+// per batch, and the GPU pays from kGpuChecksumMinBatchBytesService on (4 KiB
+// pool pages, integration_snippets --crossover: one page 8.2-8.9 µs to
+// validate instead of 13.8-15.1 and 8.9 µs to stamp instead of 19.9; faster
+// than the reference loop from 20-24 pages to validate and 28-32 to stamp).
+// The kernel holds `workgroups` CUs (16 serves 128-256 pages 10-15 % faster
+// than 4) and leaves after idle_us without a request or 2 * idle_us of life;
+// the next request starts a new one.
 void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000);
 void StopChecksumService();
-inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(96) << 10;
+inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(128) << 10;
 
 // Asynchronous batch for coroutine call sites: Submit, then Poll() from the
 // shard work loop (shard.cpp:67-130) until it returns true.  Pages must stay

@@ -194,8 +194,9 @@ int pcs_batch_destroy(pcs_batch *b);
 
 /* ---- pre-armed validate service (small read batches, opt-in) --------------
  * A launch per host batch costs ~14 µs before its first page is read.  While
- * the service is on, pcs_pages_validate_host(_ex) (and so
- * eloqstore::ValidateChecksums) serves eligible batches through a resident
+ * the service is on, pcs_pages_validate_host(_ex) and pcs_pages_stamp_host
+ * (and so eloqstore::ValidateChecksums / SetChecksums) serve eligible batches
+ * through a resident
  * kernel of `workgroups` workgroups that polls a request line in pinned host
  * memory between requests.  Eligible: XXH3, 1-256 pages, all in registered
  * regions, 16-byte aligned, page_size % 256 == 0, on the device that started

@@ -64,6 +64,31 @@ def test_service_serves_small_batches(service, P):
                 pool.pages[idx[j], P - 1] ^= 0x01
 
 
+@pytest.mark.parametrize("P", [4096, 16384])
+def test_service_stamps_small_batches(service, P):
+    """Stamp requests: the kernel writes each digest into its page header
+    (system-scope store, then the done word released after it); headers are
+    checked against the oracle, pages outside the batch are untouched."""
+    n_pool = 512 if P == 4096 else 128
+    with pcs.PagePool(n_pool, P) as pool:
+        pool.pages[:] = oracle.fill_pages(P, n_pool, 0x5E7 + P).reshape(n_pool, P)
+        pool.pages[:, :8] = 0
+        want = oracle.pages_digest(pool.pages.reshape(-1), P, 0)
+        rng = np.random.default_rng(P + 1)
+        done = np.zeros(n_pool, dtype=bool)
+        for n in (1, 3, 16, 100, 256):
+            idx = rng.permutation(n_pool)[:n]
+            s0, z0 = counters()
+            pcs.stamp_ptrs(pool.ptr(idx), P)
+            assert pcs.counter(SVC) == s0 + 1
+            done[idx] = True
+            hdr = pool.pages[:, :8].copy().view(np.uint64).ravel()
+            assert np.array_equal(hdr[done], want[done]), n
+            assert not hdr[~done].any()
+        ok, fb = pcs.validate_ptrs(pool.ptr(np.flatnonzero(done)[:256]), P)
+        assert ok.all() and fb is None
+
+
 def test_service_idle_gaps(service):
     """Requests spaced wider than the idle limit find their kernel gone and
     start the next generation; gaps near the limit may find the old one
@@ -89,8 +114,8 @@ def test_service_declines_what_it_cannot_serve(service):
         assert fb == 257 and ok.sum() == 299
         assert counters() == (s0, z0 + 1)
         pool.pages[idx[257], 10] ^= 0xFF
-        pcs.stamp_ptrs(pool.ptr(np.arange(16)), P, pcs.XXH64)
         s0, _ = counters()
+        pcs.stamp_ptrs(pool.ptr(np.arange(16)), P, pcs.XXH64)
         ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(16)), P, pcs.XXH64)
         assert ok.all() and fb is None and pcs.counter(SVC) == s0
     pages = [bytearray(oracle.fill_pages(P, 1, 0x5EA + i).tobytes()) for i in range(8)]
