@@ -242,7 +242,16 @@ __device__ __forceinline__ void xxh3_list_body(PageAt page_at, uint32_t P, uint6
         } else {
             h = xxh3_page_rt4<false>(page, P, L, stored);
         }
-        if (L.g == 0) emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, nullptr);
+        if (L.g == 0) {
+            emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, nullptr);
+            if (MODE == kStamp && ok) {
+                // small stamp batches: a done byte per page that the host
+                // polls instead of the completion signal, released after the
+                // header so it never lands first
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                st_nt(ok + pg, (uint8_t)1);
+            }
+        }
     }
 }
 

@@ -243,3 +243,31 @@ def test_zero_copy_validate_completion_forms(poll):
                 b2.close()
     finally:
         pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
+
+
+@pytest.mark.parametrize("poll", [0, 1])
+@pytest.mark.parametrize("P", [4096, 8192, 1280])
+def test_zero_copy_stamp_completion_forms(poll, P):
+    """PCS_TUNE_ZC_POLL on stamps: a zero-copy XXH3 stamp of up to 256 pages
+    completes from per-page done bytes, each released after its header (1),
+    or on the completion signal (0).  Back-to-back stamps with the pool's
+    bytes rewritten between calls: every header the call returns on must be
+    the oracle's digest of the new bytes, and pages outside it untouched."""
+    saved = pcs.get_tuning(pcs.TUNE_ZC_POLL)
+    pcs.set_tuning(pcs.TUNE_ZC_POLL, poll)
+    try:
+        with pcs.PagePool(512, P) as pool:
+            rng = np.random.default_rng(100 + poll)
+            for it in range(30):
+                n = (1, 6, 48, 128, 256, 300)[it % 6]
+                pool.pages[:] = oracle.fill_pages(P, 512, 0x57A0 + it).reshape(512, P)
+                pool.pages[:, :8] = 0
+                idx = rng.permutation(512)[:n]
+                pcs.stamp_ptrs(pool.ptr(idx), P)
+                hdr = pool.pages[:, :8].copy().view(np.uint64).ravel()
+                want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0)
+                assert np.array_equal(hdr[idx], want), (it, n)
+                rest = np.setdiff1d(np.arange(512), idx)
+                assert not hdr[rest].any()
+    finally:
+        pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
