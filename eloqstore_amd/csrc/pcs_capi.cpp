@@ -685,7 +685,7 @@ struct pcs_batch {
     std::vector<void*> stamp_pages;
     ZcBufs zc;
     bool zero_copy = false;  // in-flight batch reads registered pages in place
-    bool zc_polled = false;  // validate: completion seen from the landed verdicts (zc_poll)
+    bool zc_polled = false;  // completion seen from the landed verdicts / done bytes (zc_poll)
     uint64_t zc_landed = 0;  // verdicts seen so far
     uint64_t n = 0, P = 0, first_bad = UINT64_MAX;
     int mode = 0, state = 0;  // 0 idle, 1 in flight, 2 done, -1 failed
@@ -998,14 +998,18 @@ int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64
         for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
     hipStream_t s = b->stream;
     b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
-    b->zc_polled = mode == PCS_BATCH_VALIDATE && zc_poll();
+    // validate: completion from the landed verdicts; small zero-copy XXH3
+    // stamps: from the per-page done bytes (each released after the header
+    // and the digest word)
+    const bool poll_stamp = mode == PCS_BATCH_STAMP && b->zero_copy && algo == PCS_XXH3_64 && n <= kZcStampPollPages;
+    b->zc_polled = (mode == PCS_BATCH_VALIDATE || poll_stamp) && zc_poll();
     b->zc_landed = 0;
     if (b->zc_polled) arm_verdicts(b->zero_copy ? b->zc.h_ok : b->h_ok, n);
     if (b->zero_copy) {
         // stamp writes digests into the pages and into zc.h_dig (the digest
         // result of a stamp batch)
         e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
-                          mode == PCS_BATCH_VALIDATE ? b->zc.d_ok : nullptr, s);
+                          mode == PCS_BATCH_VALIDATE || b->zc_polled ? b->zc.d_ok : nullptr, s);
         if (e == hipSuccess) e = hipEventRecord(b->done, s);
         if (e != hipSuccess) {
             b->state = -1;

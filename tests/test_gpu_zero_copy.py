@@ -248,26 +248,43 @@ def test_zero_copy_validate_completion_forms(poll):
 @pytest.mark.parametrize("poll", [0, 1])
 @pytest.mark.parametrize("P", [4096, 8192, 1280])
 def test_zero_copy_stamp_completion_forms(poll, P):
-    """PCS_TUNE_ZC_POLL on stamps: a zero-copy XXH3 stamp of up to 256 pages
-    completes from per-page done bytes, each released after its header (1),
-    or on the completion signal (0).  Back-to-back stamps with the pool's
-    bytes rewritten between calls: every header the call returns on must be
-    the oracle's digest of the new bytes, and pages outside it untouched."""
+    """PCS_TUNE_ZC_POLL on stamps: a zero-copy XXH3 stamp of up to 128 pages
+    completes from per-page done bytes, each released after its header and
+    digest word (1), or on the completion signal (0).  Back-to-back sync
+    stamps and async batches (poll and wait) with the pool's bytes rewritten
+    between calls: every header (and an async batch's digests) must be the
+    oracle's digest of the new bytes once the call returns, and pages outside
+    the batch untouched."""
     saved = pcs.get_tuning(pcs.TUNE_ZC_POLL)
     pcs.set_tuning(pcs.TUNE_ZC_POLL, poll)
     try:
         with pcs.PagePool(512, P) as pool:
             rng = np.random.default_rng(100 + poll)
-            for it in range(30):
-                n = (1, 6, 48, 128, 256, 300)[it % 6]
-                pool.pages[:] = oracle.fill_pages(P, 512, 0x57A0 + it).reshape(512, P)
-                pool.pages[:, :8] = 0
-                idx = rng.permutation(512)[:n]
-                pcs.stamp_ptrs(pool.ptr(idx), P)
-                hdr = pool.pages[:, :8].copy().view(np.uint64).ravel()
-                want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0)
-                assert np.array_equal(hdr[idx], want), (it, n)
-                rest = np.setdiff1d(np.arange(512), idx)
-                assert not hdr[rest].any()
+            b = pcs.Batch()
+            try:
+                for it in range(36):
+                    n = (1, 6, 48, 128, 129, 300)[it % 6]
+                    form = it // 6 % 3  # sync call, async poll(), async wait()
+                    pool.pages[:] = oracle.fill_pages(P, 512, 0x57A0 + it).reshape(512, P)
+                    pool.pages[:, :8] = 0
+                    idx = rng.permutation(512)[:n]
+                    if form == 0:
+                        pcs.stamp_ptrs(pool.ptr(idx), P)
+                    else:
+                        b.submit_ptrs(pcs.Batch.STAMP, pool.ptr(idx), P)
+                        if form == 1:
+                            while not b.poll():
+                                pass
+                        else:
+                            b.wait()
+                    hdr = pool.pages[:, :8].copy().view(np.uint64).ravel()
+                    want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0)
+                    assert np.array_equal(hdr[idx], want), (it, n, form)
+                    if form:
+                        assert np.array_equal(np.array(b.result(), dtype=np.uint64), want), (it, n, form)
+                    rest = np.setdiff1d(np.arange(512), idx)
+                    assert not hdr[rest].any()
+            finally:
+                b.close()
     finally:
         pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
