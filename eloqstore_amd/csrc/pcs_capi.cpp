@@ -499,8 +499,8 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // ---------------------------------------------------------------------------
 // pre-armed validate service (pcs_service_*)
 // ---------------------------------------------------------------------------
-// One service per process, on the device current at pcs_service_start; one
-// request in flight (callers serialise on the mutex).  Requests are served by
+// One service per device, started and stopped on the calling thread's current
+// device; one request in flight per device (callers serialise on its mutex).  Requests are served by
 // a resident kernel (pcs_kernels.hip k_service) that leaves after idle_us
 // without a request or, between requests, after 2 * idle_us of life.  The
 // host tracks both clocks from its side (conservatively: the kernel starts
@@ -522,10 +522,10 @@ struct Service {
     uint32_t count = 0;            // requests posted to it
     bool live = false;             // it has been queued (it may have left since)
     clock::time_point launched, answered;
-    bool exit_hook = false;
 };
-Service g_service;
-std::atomic<bool> g_service_on{false};
+constexpr int kServiceDevices = 64;
+Service g_services[kServiceDevices];
+std::atomic<int> g_services_on{0};  // devices with a service: the validate / stamp paths look only when > 0
 
 int service_launch_locked(Service& sv) {
     ++sv.gen;
@@ -552,7 +552,7 @@ void service_post(Service& sv) {
 
 int service_stop_locked(Service& sv) {
     if (sv.device < 0) return PCS_OK;
-    g_service_on.store(false, std::memory_order_relaxed);
+    g_services_on.fetch_sub(1, std::memory_order_relaxed);
     __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);  // every queued kernel leaves at its next poll
     int cur = -1;
     const bool other = hipGetDevice(&cur) == hipSuccess && cur != sv.device;
@@ -572,8 +572,17 @@ int service_stop_locked(Service& sv) {
 // runtime tears down (handlers registered after the runtime's first use run
 // before its own destructors).
 void service_at_exit() {
-    std::lock_guard<std::mutex> lk(g_service.mu);
-    (void)service_stop_locked(g_service);
+    for (Service& sv : g_services) {
+        std::lock_guard<std::mutex> lk(sv.mu);
+        (void)service_stop_locked(sv);
+    }
+}
+
+// The calling thread's device's service slot, or null.
+Service* current_service() {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kServiceDevices) return nullptr;
+    return &g_services[dev];
 }
 
 constexpr int kNotServed = 1;  // service_run: not eligible, the caller takes the launch path
@@ -584,11 +593,11 @@ constexpr int kNotServed = 1;  // service_run: not eligible, the caller takes th
 int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok, uint64_t* first_bad) {
     if (algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
         return kNotServed;
-    Service& sv = g_service;
+    Service* svp = current_service();
+    if (!svp) return kNotServed;
+    Service& sv = *svp;
     std::lock_guard<std::mutex> lk(sv.mu);
     if (sv.device < 0) return kNotServed;
-    int dev = -1;
-    if (hipGetDevice(&dev) != hipSuccess || dev != sv.device) return kNotServed;
     if (!g_regions.translate(pages, n, P, sv.h->ptrs)) return kNotServed;
     sv.h->n = n;
     sv.h->page_size = P | (ok ? 0 : pcs::kServiceStamp);
@@ -797,7 +806,7 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
         if (first_bad) *first_bad = UINT64_MAX;
         return PCS_OK;
     }
-    if (g_service_on.load(std::memory_order_relaxed)) {
+    if (g_services_on.load(std::memory_order_relaxed) > 0) {
         if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
         const int r = service_run(pages, page_size, n_pages, algo, ok, first_bad);
         if (r != kNotServed) return r;
@@ -810,9 +819,11 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
     if (idle_us && (idle_us < 200 || idle_us > 1000000))
         return fail(PCS_ERR_INVALID, "idle_us must be 0 (1000) or in [200, 1000000]");
     if (int rc = require_device()) return rc;
-    Service& sv = g_service;
+    Service* svp = current_service();
+    if (!svp) return fail(PCS_ERR_INVALID, "no service slot for the current device");
+    Service& sv = *svp;
     std::lock_guard<std::mutex> lk(sv.mu);
-    if (sv.device >= 0) return fail(PCS_ERR_INVALID, "the validate service is already running");
+    if (sv.device >= 0) return fail(PCS_ERR_INVALID, "the validate service is already running on this device");
     int dev = -1;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking);
@@ -829,30 +840,32 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
     sv.workgroups = workgroups;
     sv.idle_us = idle_us ? idle_us : 1000;
     sv.live = false;
+    g_services_on.fetch_add(1, std::memory_order_relaxed);
     if (!sv.d) {
         (void)service_stop_locked(sv);
         return fail(PCS_ERR_HIP, "service mailbox has no device alias");
     }
-    if (!sv.exit_hook) {
-        std::atexit(service_at_exit);
-        sv.exit_hook = true;
-    }
-    g_service_on.store(true, std::memory_order_relaxed);
+    static std::once_flag hook;
+    std::call_once(hook, [] { std::atexit(service_at_exit); });
     return PCS_OK;
 }
 
 int pcs_service_stop(void) {
-    std::lock_guard<std::mutex> lk(g_service.mu);
-    return service_stop_locked(g_service);
+    Service* svp = current_service();
+    if (!svp) return PCS_OK;
+    std::lock_guard<std::mutex> lk(svp->mu);
+    return service_stop_locked(*svp);
 }
 
 int pcs_service_running(void) {
-    std::lock_guard<std::mutex> lk(g_service.mu);
-    return g_service.device >= 0 ? 1 : 0;
+    Service* svp = current_service();
+    if (!svp) return 0;
+    std::lock_guard<std::mutex> lk(svp->mu);
+    return svp->device >= 0 ? 1 : 0;
 }
 
 int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_pages, int algo) {
-    if (g_service_on.load(std::memory_order_relaxed)) {
+    if (g_services_on.load(std::memory_order_relaxed) > 0) {
         const void* const* cp = const_cast<const void* const*>(pages);
         if (int rc = check_host_batch_args(cp, page_size, n_pages, algo)) return rc;
         const int r = service_run(cp, page_size, n_pages, algo, nullptr, nullptr);

@@ -199,15 +199,18 @@ int pcs_batch_destroy(pcs_batch *b);
  * through a resident
  * kernel of `workgroups` workgroups that polls a request line in pinned host
  * memory between requests.  Eligible: XXH3, 1-256 pages, all in registered
- * regions, 16-byte aligned, page_size % 256 == 0, on the device that started
- * the service; everything else takes the launch path.  One request is in
+ * regions, 16-byte aligned, page_size % 256 == 0, called on a device whose
+ * service is on; everything else takes the launch path.  Each device has its
+ * own service: pcs_service_start / stop / running act on the calling
+ * thread's current device (pcs_set_device).  One request per device is in
  * flight at a time (calls from several threads serialise).  The kernel leaves
  * after idle_us (0 = 1000; else 200 .. 1000000) without a request and, between
  * requests, after 2 * idle_us of life, and the next request starts a new one:
  * it holds its CUs, and delays any device-synchronising HIP call of the
  * process, by at most 2 * idle_us.  Results are identical to the launch
- * path's (DESIGN.md §5).  PCS_ERR_INVALID for workgroups outside [1, 256] or
- * an idle_us out of range, or when the service is already running. */
+ * path's (DESIGN.md §5a).  PCS_ERR_INVALID for workgroups outside [1, 256] or
+ * an idle_us out of range, or when the device's service is already running.
+ * Services still running at exit are stopped by an atexit handler. */
 int pcs_service_start(int workgroups, uint32_t idle_us);
 int pcs_service_stop(void);
 int pcs_service_running(void); /* 1 while the service is on, 0 otherwise */

@@ -217,3 +217,29 @@ def test_service_lifecycle():
             ok, fb = pcs.validate_ptrs(ptrs, P)  # after stop: the launch path
             assert ok.all() and counters() == (s0, z0 + 1)
         pcs._call("pcs_service_stop")  # stopping a stopped service is fine
+
+
+def test_service_left_running_at_exit():
+    """A process that exits with its service on (no pcs_service_stop): the
+    atexit handler ends the resident kernel before the HIP runtime tears
+    down, so the process exits promptly and cleanly."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, eloqstore_amd as pcs, oracle\n"
+        "P = 4096\n"
+        "pool = pcs.PagePool(32, P)\n"
+        "pool.pages[:] = oracle.fill_pages(P, 32, 7).reshape(32, P)\n"
+        "pcs.stamp_ptrs(pool.ptr(np.arange(32)), P)\n"
+        "pcs._call('pcs_service_start', 4, 1000000)\n"  # 1 s idle: only the exit hook ends it early
+        "ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(8)), P)\n"
+        "assert ok.all() and fb is None and pcs.counter(pcs.COUNTER_SERVICE_BATCHES) == 1\n"
+        "print('served', flush=True)\n"
+    )
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "served" in r.stdout
+    assert time.perf_counter() - t0 < 60
