@@ -587,6 +587,17 @@ Service* current_service() {
 
 constexpr int kNotServed = 1;  // service_run: not eligible, the caller takes the launch path
 
+// After a failed request: end every queued kernel (stop word, then drain the
+// stream) so none can still read the request line when the next request
+// rewrites it; the next request starts a new generation.
+int service_reset_locked(Service& sv, int rc) {
+    __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(sv.stream);
+    __atomic_store_n(&sv.h->stop, 0, __ATOMIC_RELEASE);
+    sv.live = false;
+    return rc;
+}
+
 // A host validate (ok != null) or stamp (ok == null) batch through the
 // service: XXH3, registered 16-byte-aligned pages with page_size % 256 == 0,
 // 1..256 pages, on the service's device.
@@ -603,7 +614,7 @@ int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint
     sv.h->page_size = P | (ok ? 0 : pcs::kServiceStamp);
     for (uint64_t i = 0; i < n; ++i) sv.h->ok[i] = pcs::kServicePending;
     if (!service_waiting(sv, Service::clock::now()))
-        if (int rc = service_launch_locked(sv)) return rc;
+        if (int rc = service_launch_locked(sv)) return service_reset_locked(sv, rc);
     service_post(sv);
     const volatile uint32_t* v = sv.h->ok;
     uint64_t at = 0;
@@ -621,14 +632,15 @@ int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint
             // a new generation serves it again (verdicts are idempotent)
             while (at < n && v[at] != pcs::kServicePending) ++at;
             if (at == n) break;
-            if (++relaunched > 2) return fail(PCS_ERR_HIP, "validate service: request not answered");
-            if (int rc = service_launch_locked(sv)) return rc;
+            if (++relaunched > 2)
+                return service_reset_locked(sv, fail(PCS_ERR_HIP, "validate service: request not answered"));
+            if (int rc = service_launch_locked(sv)) return service_reset_locked(sv, rc);
             service_post(sv);
         } else if (q != hipErrorNotReady) {
-            return hip_fail(q, "service stream");
+            return service_reset_locked(sv, hip_fail(q, "service stream"));
         }
         if (Service::clock::now() - t0 > std::chrono::seconds(5))
-            return fail(PCS_ERR_HIP, "validate service: no answer within 5 s");
+            return service_reset_locked(sv, fail(PCS_ERR_HIP, "validate service: no answer within 5 s"));
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     sv.answered = Service::clock::now();
@@ -641,7 +653,8 @@ int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint
         if (first_bad) *first_bad = bad;
     } else {
         for (uint64_t i = 0; i < n; ++i)
-            if (sv.h->ok[i] != 1u) return fail(PCS_ERR_HIP, "validate service: stamp not confirmed");
+            if (sv.h->ok[i] != 1u)
+                return service_reset_locked(sv, fail(PCS_ERR_HIP, "validate service: stamp not confirmed"));
     }
     count(PCS_COUNTER_SERVICE_BATCHES);
     return PCS_OK;

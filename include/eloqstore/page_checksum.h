@@ -97,7 +97,8 @@ void UnregisterPagePool(void* base);
 // than the reference loop from 20-24 pages to validate and 28-32 to stamp).
 // The kernel holds `workgroups` CUs (16 serves 128-256 pages 10-15 % faster
 // than 4) and leaves after idle_us without a request or 2 * idle_us of life;
-// the next request starts a new one.
+// the next request starts a new one.  Start and stop act on the calling
+// thread's current device; each device has its own service.
 void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000);
 void StopChecksumService();
 inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(128) << 10;
