@@ -155,6 +155,7 @@ TUNE_INLINE_LIST = 11
 TUNE_MANIFEST_WIDE = 13
 TUNE_XXH64_WAVES = 15
 TUNE_ZC_POLL = 23
+TUNE_SERVICE_STREAM = 24
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -500,7 +500,8 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // pre-armed validate service (pcs_service_*)
 // ---------------------------------------------------------------------------
 // One service per device, started and stopped on the calling thread's current
-// device; one request in flight per device (callers serialise on its mutex).  Requests are served by
+// device; one request in flight per device: a call that finds the service
+// busy with another thread's request takes the launch path instead.  Requests are served by
 // a resident kernel (pcs_kernels.hip k_service) that leaves after idle_us
 // without a request or, between requests, after 2 * idle_us of life.  The
 // host tracks both clocks from its side (conservatively: the kernel starts
@@ -508,7 +509,7 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // verdicts); while it is sure, by a margin of idle_us / 4, that the kernel is
 // still waiting, a request is one mailbox write and a spin on the verdicts.
 // Otherwise it starts the next generation (queued behind the old kernel,
-// which ignores the new requests and leaves within the margin).
+// which leaves at the new generation's first request).
 struct Service {
     using clock = std::chrono::steady_clock;
     std::mutex mu;
@@ -526,6 +527,25 @@ struct Service {
 constexpr int kServiceDevices = 64;
 Service g_services[kServiceDevices];
 std::atomic<int> g_services_on{0};  // devices with a service: the validate / stamp paths look only when > 0
+
+// The service's stream.  HIP multiplexes a process's streams onto a few
+// hardware queues (GPU_MAX_HW_QUEUES, 4 here), in order within each queue, so
+// a kernel of another stream that shares the resident kernel's queue can wait
+// behind it until it leaves.  PCS_TUNE_SERVICE_STREAM = 1 (default) creates
+// the service's stream at the highest priority (HIP pools its hardware queues
+// by priority); under 4-16 threads of small batches that kept every thread
+// served (tools/lab/service_load.cpp, profiles/r03/service_load_*.txt).
+// 0: a plain stream.  A CU-masked stream (also a queue of its own) hung the
+// first time a second thread launched next to it and is not offered.
+hipError_t service_stream(hipStream_t* s) {
+    if (pcs::get_tuning(PCS_TUNE_SERVICE_STREAM) == 1) {
+        int lo = 0, hi = 0;
+        const hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (e != hipSuccess) return e;
+        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
 
 int service_launch_locked(Service& sv) {
     ++sv.gen;
@@ -607,8 +627,10 @@ int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint
     Service* svp = current_service();
     if (!svp) return kNotServed;
     Service& sv = *svp;
-    std::lock_guard<std::mutex> lk(sv.mu);
-    if (sv.device < 0) return kNotServed;
+    // busy with another thread's request: take the launch path (own stream)
+    // rather than queue behind it, so threads never starve on the one line
+    std::unique_lock<std::mutex> lk(sv.mu, std::try_to_lock);
+    if (!lk.owns_lock() || sv.device < 0) return kNotServed;
     if (!g_regions.translate(pages, n, P, sv.h->ptrs)) return kNotServed;
     sv.h->n = n;
     sv.h->page_size = P | (ok ? 0 : pcs::kServiceStamp);
@@ -839,7 +861,7 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
     if (sv.device >= 0) return fail(PCS_ERR_INVALID, "the validate service is already running on this device");
     int dev = -1;
     hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = service_stream(&sv.stream);
     if (e != hipSuccess) return hip_fail(e, "service start");
     if (hipHostMalloc(reinterpret_cast<void**>(&sv.h), sizeof(pcs::ServiceBox),
                       hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {

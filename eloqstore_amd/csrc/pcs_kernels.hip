@@ -1374,7 +1374,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 24;
+constexpr int kTuneKeys = 25;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1387,7 +1387,8 @@ constexpr int kTuneKeys = 24;
 // round 3: 22 the XXH64 direct-to-LDS segment ring (config 3 -0.8..-34 %,
 // profiles/r03/x64_glds_ab_*.txt).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
-                                      true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false};
+                                      true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
+                                      false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1402,7 +1403,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired*/ 0,
                                           /*retired*/ 0,
                                           /*retired (round 3: XXH64 direct-to-LDS ring)*/ 0,
-                                          /*zero-copy validate: completion from the verdicts themselves*/ 1};
+                                          /*zero-copy validate: completion from the verdicts themselves*/ 1,
+                                          /*validate service stream: 1 highest priority, 0 plain*/ 1};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1805,7 +1807,8 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // host starts the next generation of it when it can no longer be sure one is
 // waiting.  A kernel serves only requests of its own generation (the high 32
 // bits of seq), so a late kernel of an earlier generation never serves a
-// request twice.  8 lanes of each workgroup poll line 0 whole (x86 serves a
+// request twice, and leaves at the first request of a newer one, so the next
+// kernel (queued behind it on the stream) starts at once.  8 lanes of each workgroup poll line 0 whole (x86 serves a
 // 64-byte read of one host line as one snapshot, and the host writes seq
 // last); on a new seq the workgroup runs a system-scope acquire (the pages
 // and the rest of the list are read fresh from host memory), hashes pages
@@ -1831,8 +1834,12 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, 
             for (;;) {
                 w = __hip_atomic_load(line + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 const uint64_t w0 = __shfl(w, 0, 8);
-                if (w0 != last && (w0 >> 32) == gen) {
-                    go = 1;
+                if (w0 != last) {
+                    // a request of this generation, or one of a newer
+                    // generation: the host has moved on (every request of
+                    // this one is answered) and the next kernel, queued
+                    // behind this one, starts as soon as it leaves
+                    go = (w0 >> 32) == gen;
                     break;
                 }
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();

@@ -271,6 +271,9 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     async): complete once every verdict has
  *                                     landed in host memory (1) or on the
  *                                     launch's completion signal (0)
+ *   PCS_TUNE_SERVICE_STREAM       [1] stream of the validate service, read at
+ *                                     pcs_service_start: 1 highest priority
+ *                                     (hardware queues of its own), 0 plain
  * Keys 4, 5, 10, 12, 14 and 16-22 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -290,6 +293,7 @@ enum pcs_tune_key {
     PCS_TUNE_MANIFEST_WIDE = 13,
     PCS_TUNE_XXH64_WAVES = 15,
     PCS_TUNE_ZC_POLL = 23,
+    PCS_TUNE_SERVICE_STREAM = 24,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -34,7 +34,7 @@ VARIANTS = {
 
 @pytest.fixture
 def tuned(request):
-    keys = [k for k in range(1, 24) if pcs.get_tuning(k) >= 0]  # retired keys read -1
+    keys = [k for k in range(1, 25) if pcs.get_tuning(k) >= 0]  # retired keys read -1
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -154,7 +154,7 @@ def test_desc_mixed_with_leftovers(tuned, mode):
 
 def test_retired_tuning_keys_fail():
     """Keys of the variants retired in round 2 are refused, and read -1."""
-    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 22, 24, 99):
+    for k in (4, 5, 10, 12, 14, 16, 17, 18, 19, 20, 21, 22, 25, 99):
         assert pcs.get_tuning(k) == -1
         with pytest.raises(pcs.PcsError):
             pcs.set_tuning(k, 1)
