@@ -501,9 +501,10 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // ---------------------------------------------------------------------------
 // One service per device, started and stopped on the calling thread's current
 // device; one request in flight per device: a call that finds the service
-// busy with another thread's request takes the launch path instead.  Requests are served by
-// a resident kernel (pcs_kernels.hip k_service) that leaves after idle_us
-// without a request or, between requests, after 2 * idle_us of life.  The
+// busy with another thread's request takes the launch path instead.  Requests
+// are served by a resident kernel (pcs_kernels.hip k_service) that leaves
+// after idle_us without a request or, between requests, after 2 * idle_us of
+// life.  The
 // host tracks both clocks from its side (conservatively: the kernel starts
 // after its launch call and restarts its idle clock before the host sees the
 // verdicts); while it is sure, by a margin of idle_us / 4, that the kernel is
