@@ -33,5 +33,6 @@ def test_integration_snippets_run():
     assert "write path append=1: 10 pages stamped (reference loop)" in r.stdout
     assert "write path append=0: 40 pages stamped (reference loop)" in r.stdout
     assert "6-page scan batch on the reference loop" in r.stdout
+    assert "read path with the validate service: ok (32 and 128 pages served, 6 on the reference loop)" in r.stdout
     assert r.stdout.count("manifest record") == 2
     assert "(reference loop)" in r.stdout.split("manifest record")[1] and "(GPU)" in r.stdout.split("manifest record")[2]

@@ -28,7 +28,7 @@ LIB = os.path.join(ROOT, "eloqstore_amd", "libeloqstore_pcs.so")
 def test_every_snippet_is_used():
     blocks = gi.snippets(open(gi.DOC).read())
     assert set(blocks) == {"read_validate", "read_validate_async", "pool_extend", "write_page_stamp",
-                           "flush_batch_stamp", "manifest_calc_checksum", "replay_validate"}
+                           "flush_batch_stamp", "manifest_calc_checksum", "replay_validate", "service_start"}
     src = gi.render(open(gi.DOC).read(), open(gi.TEMPLATE).read())
     assert '#include "storage/page.h"' in src and not gi._MARK.search(src)
     for body in blocks.values():
