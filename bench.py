@@ -470,8 +470,9 @@ def host_inclusive(w: Workload, max_pages: int = 1 << 18):
 def batch_latency(pool, pageable, w: Workload):
     """Median wall time of one validate call over a read-path-sized batch
     (max_read_pages_batch = 128, kv_options.h:18-19; write batches <= 256),
-    scattered pages: staged (gather) vs zero-copy (registered pool), and the
-    async form (submit + poll spin) on the registered pool."""
+    scattered pages: staged (gather) vs zero-copy (registered pool), the
+    async form (submit + poll spin) on the registered pool, and the sync call
+    with the validate service on."""
     out = {}
     rng = np.random.default_rng(11)
     for nb in (1, 16, 128, 256):
@@ -499,6 +500,20 @@ def batch_latency(pool, pageable, w: Workload):
             ts.append(time.perf_counter() - t0)
         b.close()
         row["zero_copy_async"] = round(float(np.median(ts[20:])) * 1e6, 1)
+        # the same sync call with the validate service on
+        if w.algo == pcs.XXH3_64 and w.P % 256 == 0:
+            ok = np.empty(nb, dtype=np.uint8)
+            fb = ctypes.c_uint64()
+            served0 = pcs.counter(pcs.COUNTER_SERVICE_BATCHES)
+            ts = []
+            with pcs.ValidateService(4, 1000):
+                for _ in range(200):
+                    t0 = time.perf_counter()
+                    pcs.lib().pcs_pages_validate_host(ptrs.ctypes.data, w.P, nb, w.algo, ok.ctypes.data,
+                                                      ctypes.byref(fb))
+                    ts.append(time.perf_counter() - t0)
+            assert ok.all() and pcs.counter(pcs.COUNTER_SERVICE_BATCHES) - served0 == 200
+            row["zero_copy_service"] = round(float(np.median(ts[20:])) * 1e6, 1)
         out[str(nb)] = row
     return out
 
