@@ -245,3 +245,50 @@ def test_service_left_running_at_exit():
     assert r.returncode == 0, r.stderr[-2000:]
     assert "served" in r.stdout
     assert time.perf_counter() - t0 < 60
+
+
+def test_service_toggled_under_threads():
+    """Start and stop the service 20 times while four threads keep
+    validating: every call lands on the service or the launch path with the
+    oracle's verdicts (one corrupted page per batch), none hangs."""
+    P = 4096
+    with stamped_pool(512, P, 0x5EF) as pool:
+        bad_page = 300
+        pool.pages[bad_page, 50] ^= 0x04
+        stop = threading.Event()
+        errors, calls = [], [0] * 4
+
+        def worker(t):
+            rng = np.random.default_rng(200 + t)
+            try:
+                while not stop.is_set():
+                    n = int(rng.integers(1, 48))
+                    idx = rng.permutation(512)[:n]
+                    ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                    want = idx != bad_page
+                    if not np.array_equal(ok.astype(bool), want):
+                        errors.append((t, n))
+                    exp_fb = None if want.all() else int(np.flatnonzero(~want)[0])
+                    if fb != exp_fb:
+                        errors.append((t, n, fb, exp_fb))
+                    calls[t] += 1
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        s0 = pcs.counter(SVC)
+        try:
+            for _ in range(20):
+                pcs._call("pcs_service_start", 4, 1000)
+                time.sleep(0.01)
+                pcs._call("pcs_service_stop")
+                time.sleep(0.005)
+        finally:
+            stop.set()
+            for x in th:
+                x.join()
+        assert not errors, errors[:5]
+        assert min(calls) > 20 and pcs.counter(SVC) > s0
+        assert pcs.lib().pcs_service_running() == 0
