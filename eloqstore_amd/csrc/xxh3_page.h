@@ -429,12 +429,34 @@ __device__ __forceinline__ uint64_t xxh3_page_any(const uint8_t* __restrict__ pa
 // pages the group kernels take at all: the XXH3 long path (hashed length > 240)
 __device__ __forceinline__ bool xxh3_group_ok(uint32_t P) { return P >= 249u; }
 
-// Tile t of nb -> renumbered so that the blocks of one XCD (blockIdx % 8)
-// walk one contiguous eighth of the batch (cdna_hip_programming.md T1,
-// bijective form).
-__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t nb) {
+// Block b of a grid that covers nb tiles once -> its tile.  Blocks are
+// dispatched to the XCDs round-robin (XCD = b % 8); here each XCD takes
+// chunks of C consecutive tiles (4 MiB of 4 KiB pages at C = 64 16-page
+// tiles), and the chunks go to the XCDs round-robin, so at any moment the
+// eight XCDs stream eight adjacent chunks.  Round 1 gave each XCD one
+// contiguous eighth of the batch instead (cdna_hip_programming.md T1): on
+// large or irregular batches that made the rate depend on where the buffer
+// landed in physical memory (config 5: 0.815-0.924 over four allocations in
+// one process, config 3: 0.844-0.896), while the chunked order holds
+// 0.922-0.930 and 0.896-0.897 on the same allocations and is level or
+// better on configs 2, 4 and 7 (profiles/r03/placement_*.txt).
+// Tiles past the last whole round of chunks keep dispatch order (bijective).
+// Round 1's order: the blocks of one XCD walk one contiguous eighth of the
+// batch (cdna_hip_programming.md T1, bijective form).  Kept for the XXH64
+// LDS kernel, where it beats the chunked order (config 2 0.863 against 0.800
+// at 16-tile chunks, config 3 0.809 against 0.801, profiles/r03/
+// x64_tile_order_ab.txt), and for the manifest block sums (not re-measured).
+__device__ __forceinline__ uint64_t xcd_tile_eighths(uint64_t b, uint64_t nb) {
     const uint64_t q = nb / 8, r = nb % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <uint64_t C = 64>
+__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t nb) {
+    const uint64_t full = nb / (8 * C) * (8 * C);
+    if (b >= full) return b;
+    const uint64_t x = b % 8, k = b / 8;
+    return ((k / C) * 8 + x) * C + k % C;
 }
 
 }  // namespace pcs
