@@ -1181,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_scatter_stamp_desc(uint8_t* __restrict_
 
 // Streaming-read ceiling: the fastest plain read of a device byte range found
 // (tools/lab/stream_lab.hip, profiles/r02/read_ceiling_lab.txt): one-shot
-// workgroups over contiguous 64 KiB windows in XCD-contiguous order, the
+// workgroups over contiguous 64 KiB windows in the kernels' tile order, the
 // product's lane layout (16-lane groups over 4 KiB slices, 16 nt dwordx4 loads
 // per lane issued before any is used), folded with xor/add into one word per
 // window.  7.2-7.3 TB/s over 4-32 GiB, insensitive to workgroups per CU (2-8)
@@ -1191,7 +1191,7 @@ constexpr uint64_t kStreamWin = 65536;
 __global__ __launch_bounds__(256) void k_stream_read(const uint8_t* __restrict__ buf, uint64_t bytes,
                                                     uint64_t* __restrict__ out) {
     const uint64_t nwin = (bytes + kStreamWin - 1) / kStreamWin;
-    const uint64_t w = xcd_tile_eighths(blockIdx.x, nwin);
+    const uint64_t w = xcd_tile(blockIdx.x, nwin);
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const uint8_t* win = buf + w * kStreamWin + 4096u * grp + 16u * g;
     const uint64_t lim = bytes - w * kStreamWin;  // bytes of this window (full ones: >= 64 KiB)
