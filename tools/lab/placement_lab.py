@@ -12,7 +12,7 @@ compared across arenas.  The tile-order comparison of DESIGN.md §6a
 selected the kernels' tile order; the key was removed with the chunked order
 it chose.
 
-    python tools/lab/placement_lab.py [CONFIG]   (default 3)
+    [ALGO=xxh64] python tools/lab/placement_lab.py [CONFIG]   (default 3)
 """
 import os
 import statistics
@@ -30,14 +30,15 @@ import eloqstore_amd as pcs  # noqa: E402
 def main():
     K, R = int(os.environ.get("K", "30")), int(os.environ.get("R", "5"))
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    algo = pcs.XXH64 if os.environ.get("ALGO") == "xxh64" else pcs.XXH3_64
     dev = "cuda:0"
     arenas = {}
-    arenas["first"] = bench.Workload(cfg, pcs.XXH3_64, 0, None, dev)
+    arenas["first"] = bench.Workload(cfg, algo, 0, None, dev)
     pad4 = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
-    arenas["after_4G"] = bench.Workload(cfg, pcs.XXH3_64, 0, None, dev)
+    arenas["after_4G"] = bench.Workload(cfg, algo, 0, None, dev)
     pad16 = torch.empty(16 << 30, dtype=torch.uint8, device=dev)
-    arenas["after_20G"] = bench.Workload(cfg, pcs.XXH3_64, 0, None, dev)
-    arenas["next"] = bench.Workload(cfg, pcs.XXH3_64, 0, None, dev)
+    arenas["after_20G"] = bench.Workload(cfg, algo, 0, None, dev)
+    arenas["next"] = bench.Workload(cfg, algo, 0, None, dev)
     for name, w in arenas.items():
         print(f"{name:10s} arena at {w.pages.data_ptr():#x}", flush=True)
     times = {a: [] for a in arenas}
@@ -54,7 +55,7 @@ def main():
     for a in names:
         t = statistics.median(times[a])
         frac = arenas[a].algorithmic_bytes("digest") / t / 8e12
-        print(f"config{cfg} {a:10s} median {t * 1e6:8.1f} us  frac {frac:.4f}  rounds "
+        print(f"config{cfg} {os.environ.get('ALGO', 'xxh3')} {a:10s} median {t * 1e6:8.1f} us  frac {frac:.4f}  rounds "
               f"{[round(x * 1e6, 1) for x in times[a]]}", flush=True)
     del pad4, pad16
 
