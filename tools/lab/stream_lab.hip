@@ -44,6 +44,16 @@ __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t nb) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// Round 3's chunked order (the product's xcd_tile): each XCD takes chunks of
+// C consecutive windows, the chunks dealt to the XCDs round-robin.
+template <uint64_t C>
+__device__ __forceinline__ uint64_t xcd_chunk(uint64_t b, uint64_t nb) {
+    const uint64_t full = nb / (8 * C) * (8 * C);
+    if (b >= full) return b;
+    const uint64_t x = b % 8, k = b / 8;
+    return ((k / C) * 8 + x) * C + k % C;
+}
+
 // LAYOUT 0: instruction i of the workgroup covers bytes [i*T*16, (i+1)*T*16)
 //           of its window (each wave-instruction = 1 KiB contiguous).
 // LAYOUT 1: the product's 16-lane groups: group k of the workgroup owns the
@@ -74,6 +84,29 @@ __global__ __launch_bounds__(T) void k_win(const uint8_t* __restrict__ buf, uint
         y += d[i].y + d[i].w;
     }
     if ((x ^ y) == 0x9E3779B9u) out[w] = x;  // practically never: keeps the loads live
+}
+
+// k_win in the chunked order (C windows per chunk).
+template <int CH, int T, uint64_t C, int LAYOUT>
+__global__ __launch_bounds__(T) void k_win_c(const uint8_t* __restrict__ buf, uint64_t nwin, uint64_t* out) {
+    constexpr int L = CH / (T * 16);
+    const uint64_t w = xcd_chunk<C>(blockIdx.x, nwin);
+    const u32x4* base = reinterpret_cast<const u32x4*>(buf + w * (uint64_t)CH);
+    u32x4 d[L];
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    constexpr int G = T / 16;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        if constexpr (LAYOUT == 0) d[i] = ld<true>(base + i * T + threadIdx.x);
+        else d[i] = ld<true>(base + (grp + (i / 16) * G) * 256 + (i % 16) * 16 + g);
+    }
+    uint32_t x = 0, y = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        x ^= d[i].x ^ d[i].z;
+        y += d[i].y + d[i].w;
+    }
+    if ((x ^ y) == 0x9E3779B9u) out[w] = x;
 }
 
 // Layout 1 (the product's groups) with SLEEP x 64 cycles of s_sleep after the
@@ -196,6 +229,28 @@ int main(int argc, char** argv) {
     };
     const bool only_product = argc > 2 && std::string(argv[2]) == "product";
     const bool sleep_mode = argc > 2 && std::string(argv[2]) == "sleep";
+    const bool chunk_mode = argc > 2 && std::string(argv[2]) == "chunk";
+    for (uint64_t bytes : {uint64_t(4) << 30, big}) {
+        if (!chunk_mode) break;
+        char t[128];
+        auto nm = [&](const char* v) {
+            std::snprintf(t, sizeof t, "%-34s %6.2f GiB", v, bytes / double(1ull << 30));
+            return t;
+        };
+        add_win(nm("eighths win64K groups"), bytes, k_win<65536, 256, true, true, 1>, 65536, 256);
+        add_win(nm("chunk4M win64K groups"), bytes, k_win_c<65536, 256, 64, 1>, 65536, 256);
+        add_win(nm("chunk4M win64K L0"), bytes, k_win_c<65536, 256, 64, 0>, 65536, 256);
+        add_win(nm("chunk4M win32K groups"), bytes, k_win_c<32768, 256, 128, 1>, 32768, 256);
+        add_win(nm("chunk4M win128K groups"), bytes, k_win_c<131072, 256, 32, 1>, 131072, 256);
+        add_win(nm("chunk4M win128K T512 groups"), bytes, k_win_c<131072, 512, 32, 1>, 131072, 512);
+        add_win(nm("chunk4M win16K T64 groups"), bytes, k_win_c<16384, 64, 256, 1>, 16384, 64);
+        add_win(nm("chunk1M win64K groups"), bytes, k_win_c<65536, 256, 16, 1>, 65536, 256);
+        add_win(nm("chunk16M win64K groups"), bytes, k_win_c<65536, 256, 256, 1>, 65536, 256);
+        add_win(nm("chunk8M win128K groups"), bytes, k_win_c<131072, 256, 64, 1>, 131072, 256);
+        vs.push_back({std::string(nm("PRODUCT stream_read")), double(bytes), [=](hipStream_t s) {
+                          pcs_stream_read_dev(buf, bytes, out, (pcs_stream_t)s);
+                      }, {}});
+    }
     for (uint64_t bytes : {uint64_t(4) << 30, big}) {
         if (!sleep_mode) break;
         char t[128];
@@ -210,7 +265,7 @@ int main(int argc, char** argv) {
         add_win(nm("win64K groups sleep 64x64cyc"), bytes, k_win_sleep<64>, 65536, 256);
     }
     for (uint64_t bytes : {uint64_t(4) << 30, bytes3 & ~((uint64_t(128) << 10) - 1), big}) {
-        if (only_product || sleep_mode) break;
+        if (only_product || sleep_mode || chunk_mode) break;
         char t[128];
         auto nm = [&](const char* v) {
             std::snprintf(t, sizeof t, "%-34s %6.2f GiB", v, bytes / double(1ull << 30));
