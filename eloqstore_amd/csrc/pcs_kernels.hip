@@ -429,7 +429,7 @@ enum Addr : int { kAddrStride = 0, kAddrDesc = 1, kAddrList = 2 };
 // consecutive pages.  Sorting a tile's pages by size before handing them to
 // the waves measured 4 % slower on config 3 (profiles/r01/x64_sort_lab.txt:
 // the block is held until its all-16 KiB wave ends) and was retired in round 2.
-template <int MODE, bool NT, int ADDR, int DEPTH, int WPB = 4, int ORD = 0>
+template <int MODE, bool NT, int ADDR, int DEPTH, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                        const uint32_t* __restrict__ len, uint32_t Pfixed, uint64_t n,
                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
     const uint64_t ntiles = (n + kTile - 1) / kTile;
     const bool remap = gridDim.x == ntiles;
     for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t T = (remap ? (ORD == 0 ? xcd_tile_eighths(t0, ntiles) : xcd_tile<(uint64_t)ORD>(t0, ntiles)) : t0) * kTile;
+        const uint64_t T = (remap ? xcd_tile_eighths(t0, ntiles) : t0) * kTile;
         // page in wave slot j (0..15) of this wave
         auto page_at = [&](int j) -> uint64_t { return T + wv * 16 + j; };
         // loader pages (4ii + r) and hasher page (4i + r)
@@ -1380,7 +1380,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 26;
+constexpr int kTuneKeys = 25;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1394,7 +1394,7 @@ constexpr int kTuneKeys = 26;
 // profiles/r03/x64_glds_ab_*.txt).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, false};
+                                      false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1410,8 +1410,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired*/ 0,
                                           /*retired (round 3: XXH64 direct-to-LDS ring)*/ 0,
                                           /*zero-copy validate: completion from the verdicts themselves*/ 1,
-                                          /*validate service stream: 1 highest priority, 0 plain*/ 1,
-                                          /*LAB: xxh64 LDS tile order (0 eighths, else chunk of that many tiles)*/ 0};
+                                          /*validate service stream: 1 highest priority, 0 plain*/ 1};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1468,16 +1467,6 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
         return;
     }
 #define L(D) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
-#define LO(C) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, kX64LdsDepth, 4, C>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb)
-    const int64_t ord = g_tune[25].load(std::memory_order_relaxed);
-    if (ADDR != kAddrList && depth == kX64LdsDepth && ord != 0) {
-        if (ord == 128) LO(128);
-        else if (ord == 256) LO(256);
-        else if (ord == 512) LO(512);
-        else LO(1024);
-        return;
-    }
-#undef LO
     if (depth == 1) L(1);
     else if (depth == 2) L(2);
     else L(4);

@@ -445,7 +445,9 @@ __device__ __forceinline__ bool xxh3_group_ok(uint32_t P) { return P >= 249u; }
 // batch (cdna_hip_programming.md T1, bijective form).  Kept for the XXH64
 // LDS kernel, where it beats the chunked order (config 2 0.863 against 0.800
 // at 16-tile chunks, config 3 0.809 against 0.801, profiles/r03/
-// x64_tile_order_ab.txt).
+// x64_tile_order_ab.txt); chunks of 128-1024 of its 64-page tiles are no
+// better either (config 2 -4.5..+0.2 %, config 3 -0.3..-1.0 %, config 4
+// -12.8..+0.5 %, profiles/r03/lab_r03h/x64_order_c*.txt).
 __device__ __forceinline__ uint64_t xcd_tile_eighths(uint64_t b, uint64_t nb) {
     const uint64_t q = nb / 8, r = nb % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
