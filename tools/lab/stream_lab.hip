@@ -90,6 +90,7 @@ __global__ __launch_bounds__(T) void k_win(const uint8_t* __restrict__ buf, uint
 template <int CH, int T, uint64_t C, int LAYOUT>
 __global__ __launch_bounds__(T) void k_win_c(const uint8_t* __restrict__ buf, uint64_t nwin, uint64_t* out) {
     constexpr int L = CH / (T * 16);
+    static_assert(LAYOUT == 0 || L % 16 == 0, "layout 1 covers whole 4 KiB slices: CH must be a multiple of 256 * T");
     const uint64_t w = xcd_chunk<C>(blockIdx.x, nwin);
     const u32x4* base = reinterpret_cast<const u32x4*>(buf + w * (uint64_t)CH);
     u32x4 d[L];
@@ -240,7 +241,7 @@ int main(int argc, char** argv) {
         add_win(nm("eighths win64K groups"), bytes, k_win<65536, 256, true, true, 1>, 65536, 256);
         add_win(nm("chunk4M win64K groups"), bytes, k_win_c<65536, 256, 64, 1>, 65536, 256);
         add_win(nm("chunk4M win64K L0"), bytes, k_win_c<65536, 256, 64, 0>, 65536, 256);
-        add_win(nm("chunk4M win32K groups"), bytes, k_win_c<32768, 256, 128, 1>, 32768, 256);
+        add_win(nm("chunk4M win32K L0"), bytes, k_win_c<32768, 256, 128, 0>, 32768, 256);
         add_win(nm("chunk4M win128K groups"), bytes, k_win_c<131072, 256, 32, 1>, 131072, 256);
         add_win(nm("chunk4M win128K T512 groups"), bytes, k_win_c<131072, 512, 32, 1>, 131072, 512);
         add_win(nm("chunk4M win16K T64 groups"), bytes, k_win_c<16384, 64, 256, 1>, 16384, 64);
