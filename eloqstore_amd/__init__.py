@@ -24,6 +24,7 @@ import torch  # noqa: F401  (loads the process's HIP runtime before the library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libeloqstore_pcs.so")
+DROPIN_LIB_PATH = os.path.join(HERE, "libeloqstore_pcs_dropin.so")  # opt-in single-page C++ symbols
 TOOL_PATH = os.path.join(HERE, "page_checksum_tool")
 HEADER_PATH = os.path.join(ROOT, "include", "eloqstore_pcs.h")
 
@@ -156,11 +157,15 @@ TUNE_MANIFEST_WIDE = 13
 TUNE_XXH64_WAVES = 15
 TUNE_ZC_POLL = 23
 TUNE_SERVICE_STREAM = 24
+TUNE_SERVICE_TEAR_TEST = 25  # test only
+TUNE_FAIL_INJECT = 26  # test only
+TUNE_SERVICE_MAX_CALLERS = 27
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1
 COUNTER_GATHER_CHUNKS = 2
 COUNTER_SERVICE_BATCHES = 3
+COUNTER_SERVICE_TORN_REQUESTS = 4
 
 
 def counter(which: int) -> int:

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace pcs {
@@ -46,28 +47,54 @@ hipError_t run_manifest(const uint8_t* content, uint64_t len, uint64_t* out, hip
 hipError_t scratch_acquire(size_t bytes, void** out, int* id);
 hipError_t scratch_release(int id, hipStream_t s);
 int set_tuning(int key, int64_t value);
+// Decrements a positive knob by one and returns true (PCS_TUNE_FAIL_INJECT).
+bool take_tuning(int key);
 int64_t get_tuning(int key);
 // Plain streaming read of [buf, buf + bytes) (the HBM read ceiling): one
 // folded word per 64 KiB window into out[0 .. ceil(bytes / 65536)).
 hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s);
 
 // Pre-armed validate service (pcs_service_*): a mailbox in pinned host
-// memory, read by the waiting kernel through its device alias.  Line 0
-// carries a whole small request (seq = generation << 32 | count, page count,
-// page size and the first five page addresses), so the kernel's poll brings
-// it in with one PCIe read; the host writes `seq` last.  Verdicts are 32-bit
-// words stored system-scope.
+// memory, read by the waiting kernel through its device alias.  The first
+// kServiceLineWords words (two 64-byte lines) carry a whole small request:
+// seq = generation << 32 | count, page count, page size, a check word and the
+// first kServiceLinePtrs page addresses, so the poll that sees a new seq
+// brings in a request of up to 12 pages.  The host writes seq last.  The 16
+// words arrive as separate per-lane loads, so nothing makes them one
+// snapshot: the check word (the sum of service_word_mix over the other 15
+// words, written by the host just before seq) is what proves that a poll saw
+// one request's words and not a new seq beside an older request's page
+// addresses.  A poll whose words do not add up to their check word is
+// ignored and the line is read again.  Verdicts are 32-bit words stored
+// system-scope.
 constexpr int kServiceMaxPages = 256;
+constexpr int kServiceLineWords = 16;
+constexpr int kServiceCheckWord = 3;
+constexpr int kServiceLinePtrs = kServiceLineWords - 4;
 constexpr uint32_t kServicePending = 0xA5A5A5A5u;
 constexpr uint64_t kServiceStamp = 1ull << 32;  // in the page-size word: a stamp request
 struct ServiceBox {
     alignas(64) uint64_t seq;
     uint64_t n;
     uint64_t page_size;               // | kServiceStamp for a stamp request
+    uint64_t check;                   // sum of service_word_mix(word i, i) over the other line words
     uint64_t ptrs[kServiceMaxPages];  // device-visible page addresses
     alignas(64) uint64_t stop;        // host: 1 ends every waiting kernel
+    uint64_t torn_seq;                // kernel: the last seq it saw beside words that failed the check
     alignas(64) uint32_t ok[kServiceMaxPages];
 };
+static_assert(offsetof(ServiceBox, ptrs) == 4 * sizeof(uint64_t), "line words: seq, n, page_size, check, ptrs");
+// murmur3's 64-bit finaliser over (word, position): a word read from an older
+// request changes the sum by a pseudo-random 64-bit amount.
+__host__ __device__ inline uint64_t service_word_mix(uint64_t w, uint64_t i) {
+    uint64_t x = w ^ (i * 0x9E3779B97F4A7C15ull) ^ 0xD6E8FEB86659FD93ull;
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    x ^= x >> 33;
+    return x;
+}
 // Queue one service kernel of generation `gen`: it serves that generation's
 // requests until idle_ticks pass without one or, between requests, it has
 // lived life_ticks (both on the 100 MHz real-time clock), or stop is set.

@@ -1,5 +1,7 @@
-// page_checksum.cpp — eloqstore::SetChecksum / ValidateChecksum (+ batched
-// forms) over the C ABI.  See include/eloqstore/page_checksum.h.
+// page_checksum.cpp — the batched C++ forms of eloqstore's page checksum over
+// the C ABI (include/eloqstore/page_checksum.h).  The single-page
+// SetChecksum / ValidateChecksum live in page_checksum_dropin.cpp, a library
+// of their own, so linking this one never interposes on page.cpp's.
 #include "eloqstore/page_checksum.h"
 
 #include <cstdio>
@@ -11,10 +13,6 @@
 namespace eloqstore {
 namespace {
 
-// Digest header width: eloqstore::checksum_bytes (include/storage/page.h:11),
-// which this library's public header deliberately does not define.
-constexpr size_t kChecksumBytes = 8;
-
 [[noreturn]] void die(const char* where, int rc) {
     std::fprintf(stderr, "eloqstore page checksum: %s failed (%d): %s\n", where, rc, pcs_last_error());
     std::abort();
@@ -22,36 +20,34 @@ constexpr size_t kChecksumBytes = 8;
 
 }  // namespace
 
-void SetChecksum(std::string_view blob) {
-    if (blob.size() < kChecksumBytes) return;
-    void* page = const_cast<char*>(blob.data());
-    if (int rc = pcs_pages_stamp_host(&page, blob.size(), 1, PCS_XXH3_64)) die("SetChecksum", rc);
+int TryValidateChecksums(std::span<const char* const> pages, size_t page_size, uint8_t* ok_out, size_t* first_bad,
+                         PageHash hash, bool skip_verify) {
+    uint64_t fb = UINT64_MAX;
+    static_assert(sizeof(const char*) == sizeof(const void*));
+    const int rc = pcs_pages_validate_host_ex(reinterpret_cast<const void* const*>(pages.data()), page_size,
+                                              pages.size(), static_cast<int>(hash), ok_out, &fb,
+                                              skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE);
+    if (rc == PCS_OK && first_bad) *first_bad = fb == UINT64_MAX ? pages.size() : static_cast<size_t>(fb);
+    return rc;
 }
 
-bool ValidateChecksum(std::string_view blob) {
-    if (blob.size() < kChecksumBytes) return false;
-    const void* page = blob.data();
-    uint8_t ok = 0;
-    if (int rc = pcs_pages_validate_host(&page, blob.size(), 1, PCS_XXH3_64, &ok, nullptr))
-        die("ValidateChecksum", rc);
-    return ok != 0;
+int TrySetChecksums(std::span<char* const> pages, size_t page_size, PageHash hash) {
+    return pcs_pages_stamp_host(reinterpret_cast<void* const*>(pages.data()), page_size, pages.size(),
+                                static_cast<int>(hash));
 }
+
+const char* LastChecksumError() { return pcs_last_error(); }
 
 size_t ValidateChecksums(std::span<const char* const> pages, size_t page_size, uint8_t* ok_out, PageHash hash,
                          bool skip_verify) {
-    uint64_t first_bad = UINT64_MAX;
-    static_assert(sizeof(const char*) == sizeof(const void*));
-    if (int rc = pcs_pages_validate_host_ex(reinterpret_cast<const void* const*>(pages.data()), page_size,
-                                            pages.size(), static_cast<int>(hash), ok_out, &first_bad,
-                                            skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
+    size_t first_bad = pages.size();
+    if (int rc = TryValidateChecksums(pages, page_size, ok_out, &first_bad, hash, skip_verify))
         die("ValidateChecksums", rc);
-    return first_bad == UINT64_MAX ? pages.size() : static_cast<size_t>(first_bad);
+    return first_bad;
 }
 
 void SetChecksums(std::span<char* const> pages, size_t page_size, PageHash hash) {
-    if (int rc = pcs_pages_stamp_host(reinterpret_cast<void* const*>(pages.data()), page_size, pages.size(),
-                                      static_cast<int>(hash)))
-        die("SetChecksums", rc);
+    if (int rc = TrySetChecksums(pages, page_size, hash)) die("SetChecksums", rc);
 }
 
 void PageDigests(std::span<const char* const> pages, size_t page_size, uint64_t* digests_out, PageHash hash) {
@@ -76,52 +72,68 @@ void StopChecksumService() {
     if (int rc = pcs_service_stop()) die("StopChecksumService", rc);
 }
 
-ChecksumBatch::ChecksumBatch() {
-    if (int rc = pcs_batch_create(&batch_)) die("ChecksumBatch", rc);
-}
+ChecksumBatch::ChecksumBatch() { status_ = pcs_batch_create(&batch_); }
 
 ChecksumBatch::~ChecksumBatch() { pcs_batch_destroy(batch_); }
 
-void ChecksumBatch::SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash,
-                                   bool skip_verify) {
+int ChecksumBatch::TrySubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash,
+                                     bool skip_verify) {
+    if (status_) return status_;
     n_ = pages.size();
     validate_ = true;
     collected_ = false;
     ok_.assign(n_, 0);
-    if (int rc = pcs_batch_submit_ex(batch_, PCS_BATCH_VALIDATE, reinterpret_cast<const void* const*>(pages.data()),
-                                     page_size, n_, static_cast<int>(hash),
-                                     skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE))
-        die("ChecksumBatch::SubmitValidate", rc);
+    return pcs_batch_submit_ex(batch_, PCS_BATCH_VALIDATE, reinterpret_cast<const void* const*>(pages.data()),
+                               page_size, n_, static_cast<int>(hash),
+                               skip_verify ? PCS_FLAG_SKIP_VERIFY : PCS_FLAG_NONE);
 }
 
-void ChecksumBatch::SubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash) {
+int ChecksumBatch::TrySubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash) {
+    if (status_) return status_;
     n_ = pages.size();
     validate_ = false;
     collected_ = false;
-    if (int rc = pcs_batch_submit(batch_, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(pages.data()),
-                                  page_size, n_, static_cast<int>(hash)))
-        die("ChecksumBatch::SubmitStamp", rc);
+    return pcs_batch_submit(batch_, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(pages.data()), page_size,
+                            n_, static_cast<int>(hash));
 }
 
-void ChecksumBatch::Collect() {
-    if (collected_) return;
+void ChecksumBatch::SubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash,
+                                   bool skip_verify) {
+    if (int rc = TrySubmitValidate(pages, page_size, hash, skip_verify)) die("ChecksumBatch::SubmitValidate", rc);
+}
+
+void ChecksumBatch::SubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash) {
+    if (int rc = TrySubmitStamp(pages, page_size, hash)) die("ChecksumBatch::SubmitStamp", rc);
+}
+
+int ChecksumBatch::Collect() {
+    if (collected_) return PCS_OK;
     uint64_t fb = UINT64_MAX;
-    if (int rc = pcs_batch_result(batch_, validate_ ? ok_.data() : nullptr, nullptr, &fb))
-        die("ChecksumBatch::Collect", rc);
+    if (int rc = pcs_batch_result(batch_, validate_ ? ok_.data() : nullptr, nullptr, &fb)) return rc;
     first_bad_ = fb == UINT64_MAX ? n_ : static_cast<size_t>(fb);
     collected_ = true;
+    return PCS_OK;
+}
+
+int ChecksumBatch::TryPoll() {
+    if (status_) return status_;
+    const int rc = pcs_batch_poll(batch_);
+    if (rc == 1) {
+        if (int c = Collect()) return c;
+    }
+    return rc;
 }
 
 bool ChecksumBatch::Poll() {
-    const int rc = pcs_batch_poll(batch_);
+    const int rc = TryPoll();
     if (rc < 0) die("ChecksumBatch::Poll", rc);
-    if (rc == 1) Collect();
     return rc == 1;
 }
 
 void ChecksumBatch::Wait() {
+    if (status_) die("ChecksumBatch::Wait", status_);
     if (int rc = pcs_batch_wait(batch_)) die("ChecksumBatch::Wait", rc);
-    Collect();
+    if (int rc = Collect()) die("ChecksumBatch::Wait", rc);
 }
 
 uint64_t ManifestChecksum(std::string_view content) {

@@ -50,6 +50,10 @@ int require_device() {
 
 bool valid_algo(int algo) { return algo == PCS_XXH3_64 || algo == PCS_XXH64; }
 
+// PCS_TUNE_FAIL_INJECT (test only): the next k host-batch calls fail as a
+// HIP error would, so call sites can prove their fallback.
+bool injected_failure() { return pcs::take_tuning(PCS_TUNE_FAIL_INJECT); }
+
 int finish(hipError_t e, const char* what) { return e == hipSuccess ? PCS_OK : hip_fail(e, what); }
 
 // Fixed-stride pages: fast kernels when the shape allows, else descriptor
@@ -500,27 +504,37 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // pre-armed validate service (pcs_service_*)
 // ---------------------------------------------------------------------------
 // One service per device, started and stopped on the calling thread's current
-// device; one request in flight per device: a call that finds the service
-// busy with another thread's request takes the launch path instead.  Requests
-// are served by a resident kernel (pcs_kernels.hip k_service) that leaves
-// after idle_us without a request or, between requests, after 2 * idle_us of
-// life.  The
-// host tracks both clocks from its side (conservatively: the kernel starts
-// after its launch call and restarts its idle clock before the host sees the
-// verdicts); while it is sure, by a margin of idle_us / 4, that the kernel is
-// still waiting, a request is one mailbox write and a spin on the verdicts.
-// Otherwise it starts the next generation (queued behind the old kernel,
-// which leaves at the new generation's first request).
+// device, and one request line per device.  A request (a synchronous
+// validate / stamp call, or an asynchronous pcs_batch) claims the line with
+// an atomic flag, writes the request words, posts seq, and is answered
+// through the verdict words; the flag is released when the owner has read
+// its results.  A call that finds the line owned takes the launch path
+// instead of queueing behind it, so threads never starve on the one line.
+// Requests are served by a resident kernel (pcs_kernels.hip k_service) that
+// leaves after idle_us without a request or, between requests, after
+// 2 * idle_us of life.  The host tracks both clocks from its side
+// (conservatively: the kernel starts after its launch call and restarts its
+// idle clock before the host sees the verdicts); while it is sure, by a
+// margin of idle_us / 4, that the kernel is still waiting, a request is one
+// mailbox write and a wait on the verdicts.  Otherwise it starts the next
+// generation (queued behind the old kernel, which leaves at the new
+// generation's first request).  The mailbox is allocated at the first start
+// on a device and kept for the life of the process, so an asynchronous
+// request still in flight when the service stops can never read freed memory:
+// it finds the service off and re-runs its pages on the launch path.
 struct Service {
     using clock = std::chrono::steady_clock;
-    std::mutex mu;
-    int device = -1;
+    std::mutex mu;                 // everything below except line / callers / load; never held while waiting
+    std::atomic<int> line{0};      // 1 while a request owns the mailbox
+    std::atomic<int> callers{0};   // eligible calls in progress on this device, on either path
+    std::atomic<int> load{0};      // decaying average of `callers` seen at entry, x256
+    std::atomic<int> device{-1};   // -1: off (read without the lock by the entry points)
     int workgroups = 0;
     uint32_t idle_us = 0;
-    hipStream_t stream = nullptr;
-    pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped
+    hipStream_t stream = nullptr;  // recreated at start unless a request still owns the line
+    pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped; never freed
     pcs::ServiceBox* d = nullptr;  // its device alias
-    uint32_t gen = 0;              // generation of the newest queued kernel
+    uint32_t gen = 0;              // generation of the newest queued kernel (never reset)
     uint32_t count = 0;            // requests posted to it
     bool live = false;             // it has been queued (it may have left since)
     clock::time_point launched, answered;
@@ -536,8 +550,7 @@ std::atomic<int> g_services_on{0};  // devices with a service: the validate / st
 // the service's stream at the highest priority (HIP pools its hardware queues
 // by priority); under 4-16 threads of small batches that kept every thread
 // served (tools/lab/service_load.cpp, profiles/r03/service_load_*.txt).
-// 0: a plain stream.  A CU-masked stream (also a queue of its own) hung the
-// first time a second thread launched next to it and is not offered.
+// 0: a plain stream.  A CU-masked stream is not offered.
 hipError_t service_stream(hipStream_t* s) {
     if (pcs::get_tuning(PCS_TUNE_SERVICE_STREAM) == 1) {
         int lo = 0, hi = 0;
@@ -566,26 +579,58 @@ bool service_waiting(const Service& sv, Service::clock::time_point now) {
            now - sv.answered < std::chrono::microseconds(sv.idle_us) - margin;
 }
 
-void service_post(Service& sv) {
+// The check word of the request words as they now stand in the mailbox,
+// with `seq` in word 0 (service_word_mix, eloqstore_pcs_internal.h).
+uint64_t service_check(const pcs::ServiceBox* h, uint64_t seq) {
+    const uint64_t* w = &h->seq;
+    uint64_t c = pcs::service_word_mix(seq, 0);
+    for (int i = 1; i < pcs::kServiceLineWords; ++i)
+        if (i != pcs::kServiceCheckWord) c += pcs::service_word_mix(w[i], (uint64_t)i);
+    return c;
+}
+
+// Post the request words already in the mailbox under the next seq: the
+// check word, then seq last.
+uint64_t service_post_locked(Service& sv) {
+    const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.count;
+    sv.h->check = service_check(sv.h, seq);
     std::atomic_thread_fence(std::memory_order_release);
-    __atomic_store_n(&sv.h->seq, (uint64_t)sv.gen << 32 | ++sv.count, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.h->seq, seq, __ATOMIC_RELEASE);
+    return seq;
+}
+
+// Wait (bounded) until every kernel queued on `s` has left.
+hipError_t drain_bounded(hipStream_t s, std::chrono::milliseconds limit) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q != hipErrorNotReady) return q;
+        if (std::chrono::steady_clock::now() - t0 > limit) return hipErrorNotReady;
+        std::this_thread::yield();
+    }
+}
+
+// End every queued kernel (stop word, then a bounded drain) so none can still
+// read the request line when it is next rewritten; the next request starts a
+// new generation.
+hipError_t service_reset_locked(Service& sv) {
+    __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);
+    const hipError_t e = drain_bounded(sv.stream, std::chrono::milliseconds(2000));
+    __atomic_store_n(&sv.h->stop, 0, __ATOMIC_RELEASE);
+    sv.live = false;
+    return e;
 }
 
 int service_stop_locked(Service& sv) {
     if (sv.device < 0) return PCS_OK;
     g_services_on.fetch_sub(1, std::memory_order_relaxed);
-    __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);  // every queued kernel leaves at its next poll
     int cur = -1;
     const bool other = hipGetDevice(&cur) == hipSuccess && cur != sv.device;
     if (other) (void)hipSetDevice(sv.device);
-    const hipError_t e = hipStreamSynchronize(sv.stream);
-    (void)hipStreamDestroy(sv.stream);
-    (void)hipHostFree(sv.h);
+    sv.device = -1;  // a request in flight now re-runs on the launch path
+    const hipError_t e = service_reset_locked(sv);
     if (other) (void)hipSetDevice(cur);
-    sv.stream = nullptr;
-    sv.h = sv.d = nullptr;
-    sv.device = -1;
-    sv.live = false;
+    if (e == hipErrorNotReady) return fail(PCS_ERR_HIP, "service stop: kernels did not leave within 2 s");
     return finish(e, "service stop");
 }
 
@@ -606,81 +651,212 @@ Service* current_service() {
     return &g_services[dev];
 }
 
-constexpr int kNotServed = 1;  // service_run: not eligible, the caller takes the launch path
+constexpr int kNotServed = 1;  // not eligible or declined: the caller takes the launch path
+constexpr int kFallback = 2;   // the service could not answer (stopped, no answer in time): launch path
 
-// After a failed request: end every queued kernel (stop word, then drain the
-// stream) so none can still read the request line when the next request
-// rewrites it; the next request starts a new generation.
-int service_reset_locked(Service& sv, int rc) {
-    __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(sv.stream);
-    __atomic_store_n(&sv.h->stop, 0, __ATOMIC_RELEASE);
-    sv.live = false;
-    return rc;
+// PCS_TUNE_SERVICE_TEAR_TEST (test only): microseconds between posting seq
+// and writing the request words, so the kernel's polls see a new seq beside
+// the previous request's words; they must fail the check word and be ignored.
+constexpr int kTuneServiceTearTest = PCS_TUNE_SERVICE_TEAR_TEST;
+// PCS_TUNE_SERVICE_MAX_CALLERS: the contention gate (below).
+constexpr int kTuneServiceMaxCallers = PCS_TUNE_SERVICE_MAX_CALLERS;
+
+// Contention gate.  With several threads per GPU the one request line is
+// mostly owned by another thread, the calls that find it busy launch anyway,
+// and the resident kernel only widens the tail.  Every
+// eligible call counts itself in `callers` for its whole duration, on either
+// path, and folds the count it saw at entry into a decaying average (1/16 per
+// call); while the average exceeds PCS_TUNE_SERVICE_MAX_CALLERS + 0.5 the
+// service declines and the calls launch.  Counting calls on both paths keeps
+// the signal alive while the gate is closed, so it reopens only when the
+// callers thin out; the kernel idles out meanwhile and frees its CUs.
+void caller_enter(Service& sv) {
+    const int c = sv.callers.fetch_add(1, std::memory_order_relaxed) + 1;
+    const int a = sv.load.load(std::memory_order_relaxed);
+    sv.load.store(a + (((c << 8) - a) >> 4), std::memory_order_relaxed);  // racy by design: an estimate
+}
+void caller_leave(Service& sv) { sv.callers.fetch_sub(1, std::memory_order_relaxed); }
+
+// The calling thread's device's service when it is on (else null), counted
+// as a caller for the guard's lifetime.
+class CallerGuard {
+public:
+    explicit CallerGuard(Service* sv) : sv_(sv && sv->device >= 0 ? sv : nullptr) {
+        if (sv_) caller_enter(*sv_);
+    }
+    ~CallerGuard() {
+        if (sv_) caller_leave(*sv_);
+    }
+    Service* service() const { return sv_; }
+    CallerGuard(const CallerGuard&) = delete;
+    CallerGuard& operator=(const CallerGuard&) = delete;
+
+private:
+    Service* sv_;
+};
+
+bool service_gate_open(const Service& sv) {
+    const int64_t m = pcs::get_tuning(kTuneServiceMaxCallers);
+    return m <= 0 || sv.load.load(std::memory_order_relaxed) <= (int)(m << 8) + 128;
 }
 
-// A host validate (ok != null) or stamp (ok == null) batch through the
-// service: XXH3, registered 16-byte-aligned pages with page_size % 256 == 0,
-// 1..256 pages, on the service's device.
-int service_run(const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok, uint64_t* first_bad) {
-    if (algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
+// One request through the service, from claim to release.
+struct ServiceReq {
+    Service* sv = nullptr;  // set while the request owns the line
+    uint64_t n = 0, landed = 0, seq = 0;
+    bool stamp = false;
+    int relaunched = 0;
+    Service::clock::time_point posted, checked;
+};
+
+void service_release(ServiceReq& r) {
+    if (!r.sv) return;
+    r.sv->line.store(0, std::memory_order_release);
+    r.sv = nullptr;
+}
+
+std::atomic<uint64_t> g_torn_requests{0};
+
+// Claim the line and post a validate (stamp = false) or stamp request: XXH3,
+// registered 16-byte-aligned pages with page_size % 256 == 0, 1..256 pages, on
+// the calling thread's device with its service on and the gate open.
+// PCS_OK: posted, r owns the line.  kNotServed: nothing done.  < 0: error.
+int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64_t P, uint64_t n, int algo,
+                   bool stamp) {
+    if (!svp || algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
         return kNotServed;
-    Service* svp = current_service();
-    if (!svp) return kNotServed;
     Service& sv = *svp;
-    // busy with another thread's request: take the launch path (own stream)
-    // rather than queue behind it, so threads never starve on the one line
-    std::unique_lock<std::mutex> lk(sv.mu, std::try_to_lock);
-    if (!lk.owns_lock() || sv.device < 0) return kNotServed;
-    if (!g_regions.translate(pages, n, P, sv.h->ptrs)) return kNotServed;
-    sv.h->n = n;
-    sv.h->page_size = P | (ok ? 0 : pcs::kServiceStamp);
+    if (!service_gate_open(sv)) return kNotServed;
+    int expect = 0;
+    if (!sv.line.compare_exchange_strong(expect, 1, std::memory_order_acquire)) return kNotServed;
+    std::unique_lock<std::mutex> lk(sv.mu);
+    if (sv.device < 0) {
+        sv.line.store(0, std::memory_order_release);
+        return kNotServed;
+    }
+    const int64_t tear_us = pcs::get_tuning(kTuneServiceTearTest);
+    uint64_t local[pcs::kServiceMaxPages];
+    uint64_t* dst = tear_us > 0 ? local : sv.h->ptrs;
+    if (!g_regions.translate(pages, n, P, dst)) {
+        sv.line.store(0, std::memory_order_release);
+        return kNotServed;
+    }
+    r = ServiceReq{};
+    r.sv = &sv;
+    r.n = n;
+    r.stamp = stamp;
     for (uint64_t i = 0; i < n; ++i) sv.h->ok[i] = pcs::kServicePending;
     if (!service_waiting(sv, Service::clock::now()))
-        if (int rc = service_launch_locked(sv)) return service_reset_locked(sv, rc);
-    service_post(sv);
-    const volatile uint32_t* v = sv.h->ok;
-    uint64_t at = 0;
-    int relaunched = 0;
-    const auto t0 = Service::clock::now();
-    for (uint32_t spin = 0;; ++spin) {
-        while (at < n && v[at] != pcs::kServicePending) ++at;
-        if (at == n) break;
-        __builtin_ia32_pause();
-        if ((spin & 4095) != 4095) continue;
-        const hipError_t q = hipStreamQuery(sv.stream);
-        if (q == hipSuccess) {
-            // every queued kernel has left and this request is not fully
-            // answered (a workgroup reached its limit just before the post):
-            // a new generation serves it again (verdicts are idempotent)
-            while (at < n && v[at] != pcs::kServicePending) ++at;
-            if (at == n) break;
-            if (++relaunched > 2)
-                return service_reset_locked(sv, fail(PCS_ERR_HIP, "validate service: request not answered"));
-            if (int rc = service_launch_locked(sv)) return service_reset_locked(sv, rc);
-            service_post(sv);
-        } else if (q != hipErrorNotReady) {
-            return service_reset_locked(sv, hip_fail(q, "service stream"));
+        if (int rc = service_launch_locked(sv)) {
+            (void)service_reset_locked(sv);
+            service_release(r);
+            return rc;
         }
-        if (Service::clock::now() - t0 > std::chrono::seconds(5))
-            return service_reset_locked(sv, fail(PCS_ERR_HIP, "validate service: no answer within 5 s"));
+    const uint64_t page_word = P | (stamp ? pcs::kServiceStamp : 0);
+    if (tear_us > 0) {
+        // seq first, the request words after it, the check word last: until
+        // then every poll sees the new seq beside the previous request's words
+        const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.count;
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&sv.h->seq, seq, __ATOMIC_RELEASE);
+        std::this_thread::sleep_for(std::chrono::microseconds(tear_us));
+        std::memcpy(sv.h->ptrs, local, n * 8);
+        sv.h->n = n;
+        sv.h->page_size = page_word;
+        const uint64_t c = service_check(sv.h, seq);
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&sv.h->check, c, __ATOMIC_RELEASE);
+        r.seq = seq;
+    } else {
+        sv.h->n = n;
+        sv.h->page_size = page_word;
+        r.seq = service_post_locked(sv);
     }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    sv.answered = Service::clock::now();
-    if (ok) {
+    r.posted = r.checked = Service::clock::now();
+    return PCS_OK;
+}
+
+// Progress of a posted request (the line stays owned): 1 answered (results in
+// the mailbox), 0 pending, kFallback (the service cannot answer it: stopped,
+// or no answer in time; the caller re-runs it on the launch path and releases
+// the line), < 0 error.
+int service_progress(ServiceReq& r) {
+    Service& sv = *r.sv;
+    const volatile uint32_t* v = sv.h->ok;
+    while (r.landed < r.n && v[r.landed] != pcs::kServicePending) ++r.landed;
+    if (r.landed == r.n) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return 1;
+    }
+    const auto now = Service::clock::now();
+    if (now - r.checked < std::chrono::microseconds(50)) return 0;
+    r.checked = now;
+    const hipError_t q = hipStreamQuery(sv.stream);  // the stream outlives every line owner
+    if (q == hipErrorNotReady) {
+        if (now - r.posted < std::chrono::seconds(5)) return 0;
+        std::lock_guard<std::mutex> lk(sv.mu);
+        (void)service_reset_locked(sv);  // no answer in 5 s: a latency problem, not a failure
+        return kFallback;
+    }
+    std::lock_guard<std::mutex> lk(sv.mu);
+    if (q != hipSuccess) {
+        (void)service_reset_locked(sv);
+        return hip_fail(q, "service stream");
+    }
+    // every queued kernel has left with this request not fully answered (a
+    // workgroup reached its limit just before the post, or the service was
+    // stopped): verdicts are idempotent, so a new generation serves it again
+    while (r.landed < r.n && v[r.landed] != pcs::kServicePending) ++r.landed;
+    if (r.landed == r.n) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return 1;
+    }
+    if (sv.device < 0 || ++r.relaunched > 2) return kFallback;
+    if (int rc = service_launch_locked(sv)) {
+        (void)service_reset_locked(sv);
+        return rc;
+    }
+    r.seq = service_post_locked(sv);
+    r.posted = Service::clock::now();
+    return 0;
+}
+
+// After progress returned 1: verdicts (validate) or the done words (stamp).
+int service_collect(ServiceReq& r, uint8_t* ok, uint64_t* first_bad) {
+    Service& sv = *r.sv;
+    {
+        std::lock_guard<std::mutex> lk(sv.mu);
+        sv.answered = Service::clock::now();
+    }
+    if (__atomic_load_n(&sv.h->torn_seq, __ATOMIC_RELAXED) == r.seq)
+        g_torn_requests.fetch_add(1, std::memory_order_relaxed);
+    if (!r.stamp) {
         uint64_t bad = UINT64_MAX;
-        for (uint64_t i = 0; i < n; ++i) {
+        for (uint64_t i = 0; i < r.n; ++i) {
             ok[i] = (uint8_t)sv.h->ok[i];
             if (!ok[i] && bad == UINT64_MAX) bad = i;
         }
         if (first_bad) *first_bad = bad;
     } else {
-        for (uint64_t i = 0; i < n; ++i)
-            if (sv.h->ok[i] != 1u)
-                return service_reset_locked(sv, fail(PCS_ERR_HIP, "validate service: stamp not confirmed"));
+        for (uint64_t i = 0; i < r.n; ++i)
+            if (sv.h->ok[i] != 1u) return fail(PCS_ERR_HIP, "validate service: stamp not confirmed");
     }
     count(PCS_COUNTER_SERVICE_BATCHES);
     return PCS_OK;
+}
+
+// A synchronous host validate (ok != null) or stamp (ok == null) batch
+// through the service: PCS_OK, kNotServed (take the launch path) or < 0.
+int service_run(Service* svp, const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok,
+                uint64_t* first_bad) {
+    ServiceReq r;
+    const int s = service_submit(r, svp, pages, P, n, algo, ok == nullptr);
+    if (s != PCS_OK) return s;
+    int p;
+    while ((p = service_progress(r)) == 0) __builtin_ia32_pause();  // the sibling hyperthread may be a shard thread
+    int rc = p == 1 ? service_collect(r, ok, first_bad) : p == kFallback ? kNotServed : p;
+    service_release(r);
+    return rc;
 }
 
 // Device copy of one host buffer + a result word, for the manifest host API.
@@ -734,10 +910,26 @@ struct pcs_batch {
     uint64_t zc_landed = 0;  // verdicts seen so far
     uint64_t n = 0, P = 0, first_bad = UINT64_MAX;
     int mode = 0, state = 0;  // 0 idle, 1 in flight, 2 done, -1 failed
+    int algo = 0;
     bool all_ok = false;      // completed at submit with nothing hashed (skip_verify / empty)
+    // A batch the validate service took: the request owns the device's line
+    // until completion; its pages are kept to re-run them on the launch path
+    // if the service cannot answer (stopped meanwhile, or no answer in time).
+    ServiceReq svc;
+    bool via_service = false;          // in flight through the service
+    bool svc_results = false;          // the completed batch's results are svc_ok / svc_dig
+    Service* caller = nullptr;         // counted in this service's callers until completion
+    std::vector<const void*> svc_pages;
+    std::vector<uint8_t> svc_ok;
+    std::vector<uint64_t> svc_dig;
 };
 
 namespace {
+void batch_uncount(pcs_batch* b) {
+    if (b->caller) caller_leave(*b->caller);
+    b->caller = nullptr;
+}
+
 int batch_finalize(pcs_batch* b) {
     b->first_bad = UINT64_MAX;
     if (b->zero_copy) {  // results already in host memory, pages stamped in place
@@ -760,7 +952,115 @@ int batch_finalize(pcs_batch* b) {
         for (uint64_t i = 0; i < b->n; ++i) std::memcpy(b->stamp_pages[i], &b->h_dig[i], 8);  // EncodeFixed64
     }
     b->state = 2;
+    batch_uncount(b);
     return 1;
+}
+
+int batch_failed(pcs_batch* b, int rc) {
+    b->state = -1;
+    batch_uncount(b);
+    return rc;
+}
+
+// Launch path of an asynchronous batch (arguments checked, n > 0): zero-copy
+// over registered pages, else staged (gather or direct DMA), on the batch's
+// own stream; completion is seen by poll / wait.
+int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
+    hipError_t e = hipSuccess;
+    if (n * P > b->cap_bytes) {
+        (void)hipHostFree(b->h_pages);
+        (void)hipFree(b->d_pages);
+        b->h_pages = nullptr;
+        b->d_pages = nullptr;
+        b->cap_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_pages), n * P, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&b->d_pages), n * P) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "batch staging allocation failed");
+        b->cap_bytes = n * P;
+    }
+    if (n > b->cap_n) {
+        (void)hipHostFree(b->h_dig);
+        (void)hipFree(b->d_dig);
+        (void)hipHostFree(b->h_ok);
+        (void)hipFree(b->d_ok);
+        b->h_dig = nullptr; b->d_dig = nullptr; b->h_ok = nullptr; b->d_ok = nullptr;
+        b->cap_n = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&b->d_dig), n * 8) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&b->h_ok), n, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&b->d_ok), n) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "batch result allocation failed");
+        b->cap_n = n;
+    }
+    b->zero_copy = false;
+    b->stamp_pages.assign(n, nullptr);
+    if (mode == PCS_BATCH_STAMP)
+        for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
+    hipStream_t s = b->stream;
+    b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
+    // validate: completion from the landed verdicts; small zero-copy XXH3
+    // stamps: from the per-page done bytes (each released after the header
+    // and the digest word)
+    const bool poll_stamp = mode == PCS_BATCH_STAMP && b->zero_copy && algo == PCS_XXH3_64 && n <= kZcStampPollPages;
+    b->zc_polled = (mode == PCS_BATCH_VALIDATE || poll_stamp) && zc_poll();
+    b->zc_landed = 0;
+    if (b->zc_polled) arm_verdicts(b->zero_copy ? b->zc.h_ok : b->h_ok, n);
+    if (b->zero_copy) {
+        // stamp writes digests into the pages and into zc.h_dig (the digest
+        // result of a stamp batch)
+        e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
+                          mode == PCS_BATCH_VALIDATE || b->zc_polled ? b->zc.d_ok : nullptr, s);
+        if (e == hipSuccess) e = hipEventRecord(b->done, s);
+        if (e != hipSuccess) return hip_fail(e, "pcs_batch_submit (zero-copy)");
+        count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
+        b->state = 1;
+        return PCS_OK;
+    }
+    const bool direct = contiguous_pinned(pages, n, P);
+    if (!direct) gather(b->h_pages, pages, 0, n, P);
+    count(direct ? PCS_COUNTER_DIRECT_DMA_CHUNKS : PCS_COUNTER_GATHER_CHUNKS);
+    e = hipMemcpyAsync(b->d_pages, direct ? pages[0] : b->h_pages, n * P, hipMemcpyHostToDevice, s);
+    const int kmode = mode == PCS_BATCH_VALIDATE ? 1 : 0;
+    if (e == hipSuccess) e = pcs::run_pages(kmode, algo, b->d_pages, P, n, b->d_dig, b->d_ok, nullptr, s);
+    if (e == hipSuccess)
+        e = kmode ? hipMemcpyAsync(b->h_ok, b->d_ok, n, hipMemcpyDeviceToHost, s)
+                  : hipMemcpyAsync(b->h_dig, b->d_dig, n * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(b->done, s);
+    if (e != hipSuccess) return hip_fail(e, "pcs_batch_submit");
+    b->state = 1;
+    return PCS_OK;
+}
+
+// Progress of a batch the service took: 1 done, 0 in flight (also after it
+// was moved to the launch path), < 0 failed.
+int batch_service_poll(pcs_batch* b) {
+    const int p = service_progress(b->svc);
+    if (p == 0) return 0;
+    if (p == 1) {
+        uint64_t fb = UINT64_MAX;
+        if (b->mode == PCS_BATCH_VALIDATE) b->svc_ok.resize(b->n);
+        const int rc = service_collect(b->svc, b->mode == PCS_BATCH_VALIDATE ? b->svc_ok.data() : nullptr, &fb);
+        service_release(b->svc);
+        b->via_service = false;
+        if (rc) return batch_failed(b, rc);
+        if (b->mode == PCS_BATCH_STAMP) {  // the digests are the headers just landed
+            b->svc_dig.resize(b->n);
+            for (uint64_t i = 0; i < b->n; ++i) std::memcpy(&b->svc_dig[i], b->svc_pages[i], 8);  // DecodeFixed64
+        }
+        b->first_bad = fb;
+        b->svc_results = true;
+        b->state = 2;
+        batch_uncount(b);
+        return 1;
+    }
+    service_release(b->svc);
+    b->via_service = false;
+    if (p < 0) return batch_failed(b, p);
+    // kFallback: the same pages on the launch path
+    if (int rc = batch_launch(b, b->mode, b->svc_pages.data(), b->P, b->n, b->algo)) return batch_failed(b, rc);
+    return 0;
 }
 }  // namespace
 
@@ -842,10 +1142,13 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
         if (first_bad) *first_bad = UINT64_MAX;
         return PCS_OK;
     }
+    if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
     if (g_services_on.load(std::memory_order_relaxed) > 0) {
         if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
-        const int r = service_run(pages, page_size, n_pages, algo, ok, first_bad);
+        CallerGuard g(current_service());
+        const int r = service_run(g.service(), pages, page_size, n_pages, algo, ok, first_bad);
         if (r != kNotServed) return r;
+        return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
     }
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
 }
@@ -862,25 +1165,38 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
     if (sv.device >= 0) return fail(PCS_ERR_INVALID, "the validate service is already running on this device");
     int dev = -1;
     hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = service_stream(&sv.stream);
     if (e != hipSuccess) return hip_fail(e, "service start");
-    if (hipHostMalloc(reinterpret_cast<void**>(&sv.h), sizeof(pcs::ServiceBox),
-                      hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    // The stream is recreated (PCS_TUNE_SERVICE_STREAM is read here) unless
+    // an asynchronous request of the previous run still owns the line and
+    // may query it; the mailbox is allocated once and kept.
+    if (sv.stream && sv.line.load(std::memory_order_acquire) == 0) {
         (void)hipStreamDestroy(sv.stream);
         sv.stream = nullptr;
-        return fail(PCS_ERR_NOMEM, "service mailbox allocation failed");
     }
-    std::memset(static_cast<void*>(sv.h), 0, sizeof(pcs::ServiceBox));
-    sv.d = dev_alias(sv.h);
-    sv.device = dev;
+    if (!sv.stream && (e = service_stream(&sv.stream)) != hipSuccess) {
+        sv.stream = nullptr;
+        return hip_fail(e, "service start");
+    }
+    if (!sv.h) {
+        pcs::ServiceBox* h = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(pcs::ServiceBox),
+                          hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+            return fail(PCS_ERR_NOMEM, "service mailbox allocation failed");
+        std::memset(static_cast<void*>(h), 0, sizeof(pcs::ServiceBox));
+        pcs::ServiceBox* d = dev_alias(h);
+        if (!d) {
+            (void)hipHostFree(h);
+            return fail(PCS_ERR_HIP, "service mailbox has no device alias");
+        }
+        sv.h = h;
+        sv.d = d;
+    }
     sv.workgroups = workgroups;
     sv.idle_us = idle_us ? idle_us : 1000;
     sv.live = false;
+    sv.load.store(0, std::memory_order_relaxed);
+    sv.device = dev;
     g_services_on.fetch_add(1, std::memory_order_relaxed);
-    if (!sv.d) {
-        (void)service_stop_locked(sv);
-        return fail(PCS_ERR_HIP, "service mailbox has no device alias");
-    }
     static std::once_flag hook;
     std::call_once(hook, [] { std::atexit(service_at_exit); });
     return PCS_OK;
@@ -901,18 +1217,22 @@ int pcs_service_running(void) {
 }
 
 int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_pages, int algo) {
+    const void* const* cp = const_cast<const void* const*>(pages);
+    if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
     if (g_services_on.load(std::memory_order_relaxed) > 0) {
-        const void* const* cp = const_cast<const void* const*>(pages);
         if (int rc = check_host_batch_args(cp, page_size, n_pages, algo)) return rc;
-        const int r = service_run(cp, page_size, n_pages, algo, nullptr, nullptr);
+        CallerGuard g(current_service());
+        const int r = service_run(g.service(), cp, page_size, n_pages, algo, nullptr, nullptr);
         if (r != kNotServed) return r;
+        return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);
     }
-    return host_batch(2, const_cast<const void* const*>(pages), page_size, n_pages, algo, nullptr, nullptr, nullptr);
+    return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);
 }
 
 int pcs_pages_digest_host(const void* const* pages, uint64_t page_size, uint64_t n_pages, int algo,
                           uint64_t* digests) {
     if (n_pages && !digests) return fail(PCS_ERR_INVALID, "digests is null");
+    if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
     return host_batch(0, pages, page_size, n_pages, algo, nullptr, nullptr, digests);
 }
 
@@ -993,96 +1313,45 @@ int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64
     b->n = 0;
     b->first_bad = UINT64_MAX;
     b->all_ok = false;
+    b->svc_results = false;
     if (mode < 0 || mode > 2) return fail(PCS_ERR_INVALID, "bad batch mode");
     if (int rc = check_flags(flags)) return rc;
     if ((flags & PCS_FLAG_SKIP_VERIFY) && mode != PCS_BATCH_VALIDATE)
         return fail(PCS_ERR_INVALID, "PCS_FLAG_SKIP_VERIFY applies to validate batches only");
     if (int rc = check_host_batch_args(pages, P, n, algo)) return rc;
+    b->mode = mode;
+    b->P = P;
+    b->algo = algo;
+    b->zero_copy = false;
     if (n == 0 || (flags & PCS_FLAG_SKIP_VERIFY)) {
         // nothing to hash: complete at submit, before any staging is sized
         // (a skipped batch allocates and pins nothing; result() reports 1s)
-        b->mode = mode;
         b->n = n;
-        b->P = P;
-        b->zero_copy = false;
         b->stamp_pages.clear();
         b->all_ok = true;
         b->state = 2;
         return PCS_OK;
     }
+    if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
+    b->n = n;
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
-    hipError_t e = hipSuccess;
-    if (n * P > b->cap_bytes) {
-        (void)hipHostFree(b->h_pages);
-        (void)hipFree(b->d_pages);
-        b->h_pages = nullptr;
-        b->d_pages = nullptr;
-        b->cap_bytes = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_pages), n * P, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&b->d_pages), n * P) != hipSuccess)
-            return fail(PCS_ERR_NOMEM, "batch staging allocation failed");
-        b->cap_bytes = n * P;
-    }
-    if (n > b->cap_n) {
-        (void)hipHostFree(b->h_dig);
-        (void)hipFree(b->d_dig);
-        (void)hipHostFree(b->h_ok);
-        (void)hipFree(b->d_ok);
-        b->h_dig = nullptr; b->d_dig = nullptr; b->h_ok = nullptr; b->d_ok = nullptr;
-        b->cap_n = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&b->d_dig), n * 8) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&b->h_ok), n, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&b->d_ok), n) != hipSuccess)
-            return fail(PCS_ERR_NOMEM, "batch result allocation failed");
-        b->cap_n = n;
-    }
-    b->mode = mode;
-    b->n = n;
-    b->P = P;
-    b->zero_copy = false;
-    b->stamp_pages.assign(n, nullptr);
-    if (mode == PCS_BATCH_STAMP)
-        for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
-    hipStream_t s = b->stream;
-    b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
-    // validate: completion from the landed verdicts; small zero-copy XXH3
-    // stamps: from the per-page done bytes (each released after the header
-    // and the digest word)
-    const bool poll_stamp = mode == PCS_BATCH_STAMP && b->zero_copy && algo == PCS_XXH3_64 && n <= kZcStampPollPages;
-    b->zc_polled = (mode == PCS_BATCH_VALIDATE || poll_stamp) && zc_poll();
-    b->zc_landed = 0;
-    if (b->zc_polled) arm_verdicts(b->zero_copy ? b->zc.h_ok : b->h_ok, n);
-    if (b->zero_copy) {
-        // stamp writes digests into the pages and into zc.h_dig (the digest
-        // result of a stamp batch)
-        e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
-                          mode == PCS_BATCH_VALIDATE || b->zc_polled ? b->zc.d_ok : nullptr, s);
-        if (e == hipSuccess) e = hipEventRecord(b->done, s);
-        if (e != hipSuccess) {
-            b->state = -1;
-            return hip_fail(e, "pcs_batch_submit (zero-copy)");
+    if (mode != PCS_BATCH_DIGEST && g_services_on.load(std::memory_order_relaxed) > 0) {
+        Service* svp = current_service();
+        if (svp && svp->device >= 0) {
+            b->caller = svp;  // counted until the batch completes, on either path
+            caller_enter(*svp);
+            const int r = service_submit(b->svc, svp, pages, P, n, algo, mode == PCS_BATCH_STAMP);
+            if (r == PCS_OK) {
+                b->svc_pages.assign(pages, pages + n);
+                b->via_service = true;
+                b->state = 1;
+                return PCS_OK;
+            }
+            if (r < 0) return batch_failed(b, r);
         }
-        count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
-        b->state = 1;
-        return PCS_OK;
     }
-    const bool direct = contiguous_pinned(pages, n, P);
-    if (!direct) gather(b->h_pages, pages, 0, n, P);
-    count(direct ? PCS_COUNTER_DIRECT_DMA_CHUNKS : PCS_COUNTER_GATHER_CHUNKS);
-    e = hipMemcpyAsync(b->d_pages, direct ? pages[0] : b->h_pages, n * P, hipMemcpyHostToDevice, s);
-    const int kmode = mode == PCS_BATCH_VALIDATE ? 1 : 0;
-    if (e == hipSuccess) e = pcs::run_pages(kmode, algo, b->d_pages, P, n, b->d_dig, b->d_ok, nullptr, s);
-    if (e == hipSuccess)
-        e = kmode ? hipMemcpyAsync(b->h_ok, b->d_ok, n, hipMemcpyDeviceToHost, s)
-                  : hipMemcpyAsync(b->h_dig, b->d_dig, n * 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipEventRecord(b->done, s);
-    if (e != hipSuccess) {
-        b->state = -1;
-        return hip_fail(e, "pcs_batch_submit");
-    }
-    b->state = 1;
+    if (int rc = batch_launch(b, mode, pages, P, n, algo)) return batch_failed(b, rc);
     return PCS_OK;
 }
 
@@ -1090,6 +1359,15 @@ int pcs_batch_poll(pcs_batch* b) {
     if (!b) return fail(PCS_ERR_INVALID, "batch is null");
     if (b->state == 2) return 1;
     if (b->state != 1) return fail(PCS_ERR_INVALID, "no batch submitted");
+    if (b->via_service) {
+        const int r = batch_service_poll(b);
+        if (r != 0 || b->via_service || b->state != 1) return r;
+        // moved to the launch path: fall through to its completion check
+    }
+    if (injected_failure()) {
+        (void)hipStreamSynchronize(b->stream);  // nothing of this batch left in flight
+        return batch_failed(b, fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)"));
+    }
     if (b->zc_polled) {
         b->zc_landed = verdicts_landed(b->zero_copy ? b->zc.h_ok : b->h_ok, b->zc_landed, b->n);
         if (b->zc_landed == b->n) {
@@ -1099,10 +1377,7 @@ int pcs_batch_poll(pcs_batch* b) {
     }
     const hipError_t e = hipEventQuery(b->done);
     if (e == hipErrorNotReady) return 0;
-    if (e != hipSuccess) {
-        b->state = -1;
-        return hip_fail(e, "pcs_batch_poll");
-    }
+    if (e != hipSuccess) return batch_failed(b, hip_fail(e, "pcs_batch_poll"));
     return batch_finalize(b);
 }
 
@@ -1110,12 +1385,19 @@ int pcs_batch_wait(pcs_batch* b) {
     if (!b) return fail(PCS_ERR_INVALID, "batch is null");
     if (b->state == 2) return PCS_OK;
     if (b->state != 1) return fail(PCS_ERR_INVALID, "no batch submitted");
+    while (b->via_service) {
+        const int r = batch_service_poll(b);
+        if (r < 0) return r;
+        if (r == 1) return PCS_OK;
+        if (b->via_service) __builtin_ia32_pause();
+    }
+    if (injected_failure()) {
+        (void)hipStreamSynchronize(b->stream);
+        return batch_failed(b, fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)"));
+    }
     const hipError_t e = b->zc_polled ? wait_verdicts(b->zero_copy ? b->zc.h_ok : b->h_ok, b->n, b->stream)
                                       : hipEventSynchronize(b->done);
-    if (e != hipSuccess) {
-        b->state = -1;
-        return hip_fail(e, "pcs_batch_wait");
-    }
+    if (e != hipSuccess) return batch_failed(b, hip_fail(e, "pcs_batch_wait"));
     batch_finalize(b);
     return PCS_OK;
 }
@@ -1127,12 +1409,12 @@ int pcs_batch_result(pcs_batch* b, uint8_t* ok, uint64_t* digests, uint64_t* fir
         if (b->mode != PCS_BATCH_VALIDATE) return fail(PCS_ERR_INVALID, "verdicts exist only in validate mode");
         if (b->all_ok)
             std::memset(ok, 1, b->n);
-        else
-            std::memcpy(ok, b->h_ok, b->n);
+        else if (b->n)
+            std::memcpy(ok, b->svc_results ? b->svc_ok.data() : b->h_ok, b->n);
     }
     if (digests) {
         if (b->mode == PCS_BATCH_VALIDATE) return fail(PCS_ERR_INVALID, "digests exist in digest/stamp mode");
-        if (b->n) std::memcpy(digests, b->h_dig, b->n * 8);
+        if (b->n) std::memcpy(digests, b->svc_results ? b->svc_dig.data() : b->h_dig, b->n * 8);
     }
     if (first_bad) *first_bad = b->first_bad;
     return PCS_OK;
@@ -1140,6 +1422,12 @@ int pcs_batch_result(pcs_batch* b, uint8_t* ok, uint64_t* digests, uint64_t* fir
 
 int pcs_batch_destroy(pcs_batch* b) {
     if (!b) return PCS_OK;
+    if (b->via_service) {  // the request owns the device's line: see it answered (or given up) first
+        while (service_progress(b->svc) == 0) __builtin_ia32_pause();
+        service_release(b->svc);
+        b->via_service = false;
+    }
+    batch_uncount(b);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     (void)hipHostFree(b->h_pages);
     (void)hipFree(b->d_pages);
@@ -1198,6 +1486,7 @@ int pcs_set_tuning(int key, int64_t value) {
 int64_t pcs_get_tuning(int key) { return pcs::get_tuning(key); }
 
 uint64_t pcs_counter(int which) {
+    if (which == PCS_COUNTER_SERVICE_TORN_REQUESTS) return g_torn_requests.load(std::memory_order_relaxed);
     return (which < 0 || which > 3) ? 0 : g_counters[which].load(std::memory_order_relaxed);
 }
 

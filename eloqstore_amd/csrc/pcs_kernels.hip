@@ -1380,7 +1380,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 25;
+constexpr int kTuneKeys = 28;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1394,7 +1394,7 @@ constexpr int kTuneKeys = 25;
 // profiles/r03/x64_glds_ab_*.txt).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false};
+                                      false, false, false, false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1410,12 +1410,22 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired*/ 0,
                                           /*retired (round 3: XXH64 direct-to-LDS ring)*/ 0,
                                           /*zero-copy validate: completion from the verdicts themselves*/ 1,
-                                          /*validate service stream: 1 highest priority, 0 plain*/ 1};
+                                          /*validate service stream: 1 highest priority, 0 plain*/ 1,
+                                          /*test only: validate service torn-line drill, microseconds*/ 0,
+                                          /*test only: host-batch calls left to fail*/ 0,
+                                          /*validate service contention gate: callers (0 = off)*/ 2};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
     g_tune[key].store(value, std::memory_order_relaxed);
     return 0;
+}
+bool take_tuning(int key) {
+    if (key <= 0 || key >= kTuneKeys || kRetired[key]) return false;
+    int64_t v = g_tune[key].load(std::memory_order_relaxed);
+    while (v > 0)
+        if (g_tune[key].compare_exchange_weak(v, v - 1, std::memory_order_relaxed)) return true;
+    return false;
 }
 int64_t get_tuning(int key) {
     return (key <= 0 || key >= kTuneKeys || kRetired[key]) ? -1 : g_tune[key].load(std::memory_order_relaxed);
@@ -1814,64 +1824,78 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // waiting.  A kernel serves only requests of its own generation (the high 32
 // bits of seq), so a late kernel of an earlier generation never serves a
 // request twice, and leaves at the first request of a newer one, so the next
-// kernel (queued behind it on the stream) starts at once.  8 lanes of each workgroup poll line 0 whole (x86 serves a
-// 64-byte read of one host line as one snapshot, and the host writes seq
-// last); on a new seq the workgroup runs a system-scope acquire (the pages
-// and the rest of the list are read fresh from host memory), hashes pages
-// blockIdx.x * 16 + group, stride gridDim.x * 16 (the run-time-size XXH3
-// body: registered 16-byte-aligned pages, page_size % 256 == 0) and stores
-// each verdict word system-scope, which reaches host memory without a
-// release fence.  A stamp request (high half of the page-size word) stores
-// the digest into the page header instead and then a done word, released
-// after it.
+// kernel (queued behind it on the stream) starts at once.  16 lanes of each
+// workgroup poll the request words (eloqstore_pcs_internal.h: seq, n,
+// page_size, check, ptrs[0..12)) with one 8-byte load each.  Those loads are
+// separate, so a poll can see the new seq beside an older request's words:
+// the workgroup serves a request only when the 15 words' mixes add up to the
+// check word the host wrote with them, and otherwise reads the line again
+// (a torn view of one request is ignored, never served).  Then it runs a
+// system-scope acquire (pages and ptrs[12..n) are read fresh from host memory,
+// ordered after the seq that announced them), hashes pages blockIdx.x * 16 +
+// group, stride gridDim.x * 16 (the run-time-size XXH3 body: registered
+// 16-byte-aligned pages, page_size % 256 == 0) and stores each verdict word
+// system-scope, which reaches host memory without a release fence.  A stamp
+// request (high half of the page-size word) stores the digest into the page
+// header instead and then a done word, released after it.
 __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, uint64_t idle_ticks,
                                                  uint64_t life_ticks) {
-    __shared__ uint64_t s_line[8];
+    constexpr int W = kServiceLineWords;
+    __shared__ uint64_t s_line[W];
     __shared__ int s_go;
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
     uint64_t t_last = born;
     uint64_t last = gen << 32;  // this generation's requests carry gen << 32 | count, count from 1
+    uint64_t torn_noted = 0;
     for (;;) {
-        if (threadIdx.x < 8) {
+        if (threadIdx.x < W) {
             const uint64_t* line = &box->seq;
             uint64_t w = 0;
             int go = 0;
             for (;;) {
                 w = __hip_atomic_load(line + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const uint64_t w0 = __shfl(w, 0, 8);
+                const uint64_t w0 = __shfl(w, 0, W);
                 if (w0 != last) {
-                    // a request of this generation, or one of a newer
-                    // generation: the host has moved on (every request of
-                    // this one is answered) and the next kernel, queued
-                    // behind this one, starts as soon as it leaves
-                    go = (w0 >> 32) == gen;
-                    break;
+                    // a request of a newer generation: the host has moved on
+                    // (every request of this one is answered) and the next
+                    // kernel, queued behind this one, starts once it leaves
+                    if ((w0 >> 32) != gen) break;
+                    uint64_t m = threadIdx.x == kServiceCheckWord ? 0 : service_word_mix(w, threadIdx.x);
+#pragma unroll
+                    for (int d = 1; d < W; d <<= 1) m += __shfl_xor(m, d, W);
+                    if (m == __shfl(w, kServiceCheckWord, W)) {
+                        go = 1;
+                        break;
+                    }
+                    // torn: seq is new, some word is not yet this request's
+                    if (blockIdx.x == 0 && threadIdx.x == 0 && torn_noted != w0) {
+                        torn_noted = w0;
+                        __hip_atomic_store(&box->torn_seq, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                 }
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
                 if (__hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
                     now - t_last > idle_ticks || now - born > life_ticks)
                     break;
             }
+            // acquire here, in the lanes whose loads saw the new seq; the
+            // barrier then orders every lane's reads after it
+            if (go) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             s_line[threadIdx.x] = w;
             if (threadIdx.x == 0) s_go = go;
         }
         __syncthreads();
-        if (!s_go) return;  // uniform per workgroup: idle, lifetime or stop
+        if (!s_go) return;  // uniform per workgroup: idle, lifetime, stop or a newer generation
         last = s_line[0];
         const uint64_t n = s_line[1];
         const uint32_t P = (uint32_t)s_line[2];
         const bool stamp = (s_line[2] >> 32) != 0;  // kServiceStamp: write the digest into the header
-        uint64_t head[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) head[k] = s_line[3 + k];
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         for (uint64_t pg = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 4); pg < n; pg += (uint64_t)gridDim.x * 16) {
-            uint64_t a = 0;
-#pragma unroll
-            for (int k = 0; k < 5; ++k)
-                if (pg == (uint64_t)k) a = head[k];
-            if (pg >= 5) a = __hip_atomic_load(&box->ptrs[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t a = pg < (uint64_t)kServiceLinePtrs
+                                   ? s_line[4 + pg]  // came with the checked poll
+                                   : __hip_atomic_load(&box->ptrs[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             uint64_t stored = 0;
             const uint64_t h = xxh3_page_rt4<false>(reinterpret_cast<const uint8_t*>(a), P, L, stored);
             if (L.g == 0) {

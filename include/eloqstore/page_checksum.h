@@ -14,13 +14,22 @@
 // blob.size() >= 8 is assumed exactly as in the reference (a shorter blob
 // never validates and SetChecksum leaves it untouched); SetChecksum writes the
 // little-endian digest into blob[0, 8) through const_cast, as page.cpp does.
-// No exceptions: a GPU failure terminates the process with a message (the
-// reference's functions cannot fail, and a silent `false` would be reported
-// by callers as KvError::Corrupted).
+// The two single-page functions are defined ONLY in the opt-in
+// libeloqstore_pcs_dropin.so (for a store that deletes page.cpp's bodies);
+// the batch library libeloqstore_pcs.so does not export them, so a store that
+// keeps page.cpp's CPU definitions (the recommended integration,
+// INTEGRATION.md §2.4) resolves them to page.cpp in any link or DSO order.
+// They terminate the process on a GPU failure (the reference's functions
+// cannot fail, and a silent `false` would be reported by callers as
+// KvError::Corrupted).
 //
 // Batched forms for the natural batch points of the callers
 // (IouringMgr::ReadPages, async_io_manager.cpp:353-366; FlushBatchPages,
-// write_task.cpp:155-167) — scattered pool pages of one page size.
+// write_task.cpp:155-167) — scattered pool pages of one page size — in two
+// flavours: the Try* forms return a status (PCS_OK or a negative pcs_status,
+// message in LastChecksumError()) so a call site can fall back to the
+// reference's per-page loop on a GPU failure, and
+// the plain forms terminate with the message instead.
 #pragma once
 
 #include <cstddef>
@@ -65,6 +74,17 @@ inline bool GpuChecksumPays(size_t n_pages, size_t page_size, size_t min_bytes =
 // 2.8 ms on one core, 1.44 ms on the GPU).
 inline constexpr size_t kGpuManifestMinBytes = size_t(6) << 20;
 
+// Non-aborting forms.  Return PCS_OK (0) or a negative pcs_status
+// (include/eloqstore_pcs.h) with the message in LastChecksumError(); on
+// PCS_OK, *first_bad (if given) is the first corrupted index or pages.size().
+// A failed call has written nothing a caller may trust: the read path falls
+// back to page.cpp's ValidateChecksum loop, as the reference would run it
+// (async_io_manager.cpp:353-366), and the write path to SetChecksum.
+int TryValidateChecksums(std::span<const char* const> pages, size_t page_size, uint8_t* ok_out, size_t* first_bad,
+                         PageHash hash = PageHash::XXH3_64, bool skip_verify = false);
+int TrySetChecksums(std::span<char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
+const char* LastChecksumError();  // the calling thread's last failure (pcs_last_error)
+
 // Validates every page; ok_out[i] = 1 if page i's stored digest matches.
 // Returns the index of the first corrupted page, or pages.size() if all match
 // (the reference loop stops at the first failure, async_io_manager.cpp:357-363;
@@ -89,15 +109,19 @@ void RegisterPagePool(void* base, size_t bytes);
 void UnregisterPagePool(void* base);
 
 // Pre-armed validate service (pcs_service_start, opt-in): while it is on,
-// ValidateChecksums and SetChecksums serve batches of up to 256 registered
-// pages through a resident kernel polling a request line, instead of a launch
-// per batch, and the GPU pays from kGpuChecksumMinBatchBytesService on (4 KiB
-// pool pages, integration_snippets --crossover: one page 8.2-8.9 µs to
-// validate instead of 13.8-15.1 and 8.9 µs to stamp instead of 19.9; faster
-// than the reference loop from 20-24 pages to validate and 28-32 to stamp).
-// The kernel holds `workgroups` CUs (16 serves 128-256 pages 10-15 % faster
-// than 4) and leaves after idle_us without a request or 2 * idle_us of life;
-// the next request starts a new one.  Start and stop act on the calling
+// ValidateChecksums, SetChecksums and ChecksumBatch's validate and stamp
+// batches of up to 256 registered pages are served through a resident kernel
+// polling a request line, instead of a launch per batch, and the GPU pays
+// from kGpuChecksumMinBatchBytesService on (4 KiB pool pages,
+// integration_snippets --crossover: one page 8.2-8.9 µs to validate instead
+// of 13.8-15.1 and 8.9 µs to stamp instead of 19.9; faster than the reference
+// loop from 20-24 pages to validate and 28-32 to stamp).  The kernel holds
+// `workgroups` CUs (16 serves 128-256 pages 10-15 % faster than 4) and
+// leaves after idle_us without a request or 2 * idle_us of life; the next
+// request starts a new one.  One request line per device: a call that finds
+// it owned, or that arrives while more than PCS_TUNE_SERVICE_MAX_CALLERS
+// eligible calls are in progress on the device (a decaying average; 2 by
+// default), takes the launch path.  Start and stop act on the calling
 // thread's current device; each device has its own service.
 void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000);
 void StopChecksumService();
@@ -106,9 +130,11 @@ inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(128) << 10;
 // Asynchronous batch for coroutine call sites: Submit, then Poll() from the
 // shard work loop (shard.cpp:67-130) until it returns true.  Pages must stay
 // valid until then; SubmitStamp writes the digests into them on completion.
+// With the validate service on, an eligible batch is posted to it (no
+// launch) and Poll() watches its verdict words.
 class ChecksumBatch {
 public:
-    ChecksumBatch();
+    ChecksumBatch();  // never aborts: a failed creation is Status(), and every call reports it
     ~ChecksumBatch();
     ChecksumBatch(const ChecksumBatch&) = delete;
     ChecksumBatch& operator=(const ChecksumBatch&) = delete;
@@ -120,14 +146,22 @@ public:
     void SubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
     bool Poll();  // true once complete; never blocks
     void Wait();
+    // Non-aborting forms: PCS_OK / a negative pcs_status (TrySubmit*), and
+    // 1 complete / 0 in flight / a negative pcs_status (TryPoll).
+    int TrySubmitValidate(std::span<const char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64,
+                          bool skip_verify = false);
+    int TrySubmitStamp(std::span<char* const> pages, size_t page_size, PageHash hash = PageHash::XXH3_64);
+    int TryPoll();
+    int Status() const { return status_; }  // PCS_OK, or why the batch could not be created
     // Validate mode, after completion: index of the first corrupted page, or
     // the batch size if every page matched.
     size_t FirstBad() const { return first_bad_; }
     const uint8_t* Verdicts() const { return ok_.data(); }
 
 private:
-    void Collect();
+    int Collect();
     ::pcs_batch* batch_ = nullptr;
+    int status_ = 0;
     std::vector<uint8_t> ok_;
     size_t n_ = 0, first_bad_ = 0;
     bool validate_ = false, collected_ = false;

@@ -267,13 +267,30 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     per chunk (0 = one workgroup per chunk)
  *   PCS_TUNE_XXH64_WAVES          [4] waves per workgroup of the XXH64 LDS
  *                                     kernel (1, 2 or 4; 16 pages per wave)
- *   PCS_TUNE_ZC_POLL              [1] zero-copy validate batches (sync and
- *                                     async): complete once every verdict has
- *                                     landed in host memory (1) or on the
- *                                     launch's completion signal (0)
+ *   PCS_TUNE_ZC_POLL              [1] validate batches from host memory, sync
+ *                                     and async, zero-copy AND staged (gather
+ *                                     or direct DMA), plus zero-copy XXH3
+ *                                     stamps of <= 128 pages: complete once
+ *                                     every verdict / done byte has landed in
+ *                                     host memory (1) or on the launch's
+ *                                     completion signal (0)
  *   PCS_TUNE_SERVICE_STREAM       [1] stream of the validate service, read at
  *                                     pcs_service_start: 1 highest priority
  *                                     (hardware queues of its own), 0 plain
+ *   PCS_TUNE_SERVICE_MAX_CALLERS  [2] validate service contention gate: while
+ *                                     the decaying average of concurrent
+ *                                     eligible calls on the device exceeds
+ *                                     this + 0.5, the service declines and
+ *                                     calls take the launch path; 0 = off
+ *   PCS_TUNE_SERVICE_TEAR_TEST    [0] test only: microseconds the service's
+ *                                     host side waits between posting seq and
+ *                                     writing the request words (the kernel
+ *                                     must ignore the torn line meanwhile)
+ *   PCS_TUNE_FAIL_INJECT          [0] test only: the next k host-batch calls
+ *                                     (pcs_pages_*_host, pcs_batch_submit*,
+ *                                     pcs_batch_poll / wait,
+ *                                     pcs_manifest_*_host) fail with
+ *                                     PCS_ERR_HIP; decremented per failure
  * Keys 4, 5, 10, 12, 14 and 16-22 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -294,6 +311,9 @@ enum pcs_tune_key {
     PCS_TUNE_XXH64_WAVES = 15,
     PCS_TUNE_ZC_POLL = 23,
     PCS_TUNE_SERVICE_STREAM = 24,
+    PCS_TUNE_SERVICE_TEAR_TEST = 25,
+    PCS_TUNE_FAIL_INJECT = 26,
+    PCS_TUNE_SERVICE_MAX_CALLERS = 27,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
@@ -304,7 +324,9 @@ enum pcs_counter {
     PCS_COUNTER_ZERO_COPY_LAUNCHES = 0, /* registered pages hashed in place */
     PCS_COUNTER_DIRECT_DMA_CHUNKS = 1,  /* contiguous pinned runs DMA'd as is */
     PCS_COUNTER_GATHER_CHUNKS = 2,      /* pages gathered into pinned staging */
-    PCS_COUNTER_SERVICE_BATCHES = 3,    /* validate batches served by the pre-armed service */
+    PCS_COUNTER_SERVICE_BATCHES = 3,    /* validate / stamp batches served by the pre-armed service */
+    PCS_COUNTER_SERVICE_TORN_REQUESTS = 4, /* served requests whose line the kernel first saw torn
+                                              (new seq, words failing the check word) and ignored */
 };
 uint64_t pcs_counter(int which); /* 0 for an unknown counter */
 

@@ -1,0 +1,198 @@
+// service_threads_test.cpp — TEST INFRASTRUCTURE: the validate service under
+// real native concurrency (Python threads serialise on the GIL between
+// calls, so they never keep eight calls in flight at once).
+//
+// T threads of the shard-loop shape each own a disjoint range of a
+// registered page pool and issue small batches back to back:
+//   1. validate, gate off (PCS_TUNE_SERVICE_MAX_CALLERS = 0): every request
+//      carries a corrupted page of its own at a random slot (mostly the
+//      slots whose addresses come with the polled request words); each
+//      thread must get exactly its own verdicts and first_bad, on whichever
+//      path served it;
+//   2. the same through ChecksumBatch (async submit + poll), one per thread;
+//   3. stamps of disjoint pages: headers against the oracle, pages no
+//      request named keep a zero header;
+//   4. the contention gate at its default (2): one thread is always served;
+//      eight threads drive the caller average over the limit and the service
+//      declines nearly everything (launch path), verdicts exact.
+// The CPU oracle is the checker.  Prints "service threads ok" on success.
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "eloqstore/page_checksum.h"
+#include "eloqstore_pcs.h"
+#include "xxh_oracle.h"
+
+#define CHECK(c)                                                                 \
+    do {                                                                         \
+        if (!(c)) {                                                              \
+            std::fprintf(stderr, "%s:%d CHECK(%s)\n", __FILE__, __LINE__, #c);   \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+namespace {
+using Clock = std::chrono::steady_clock;
+constexpr size_t P = 4096, PER = 512;
+
+uint64_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct Counts {
+    uint64_t served, launched;
+};
+Counts counts() {
+    return {pcs_counter(PCS_COUNTER_SERVICE_BATCHES), pcs_counter(PCS_COUNTER_ZERO_COPY_LAUNCHES)};
+}
+
+// n distinct pages of thread t's range, slot k corrupted (byte flipped)
+struct Req {
+    std::vector<const char*> ptrs;
+    size_t k = 0, byte = 0;
+};
+Req make_req(char* pool, int t, uint64_t& rng, size_t max_n) {
+    Req r;
+    const size_t n = 1 + splitmix(rng) % max_n;
+    std::vector<size_t> pick;
+    while (pick.size() < n) {
+        const size_t p = splitmix(rng) % PER;
+        bool dup = false;
+        for (size_t q : pick) dup |= q == p;
+        if (!dup) pick.push_back(p);
+    }
+    for (size_t p : pick) r.ptrs.push_back(pool + (t * PER + p) * P);
+    r.k = (splitmix(rng) % 10 < 7) ? splitmix(rng) % std::min<size_t>(n, 12) : splitmix(rng) % n;
+    r.byte = 8 + splitmix(rng) % (P - 8);
+    return r;
+}
+
+int run_validate(char* pool, int T, double secs, bool async, size_t max_n, std::atomic<uint64_t>& calls) {
+    std::atomic<int> errors{0};
+    const auto stop = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(secs));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            uint64_t rng = 0xC0DE00ull + t * 7919ull + (async ? 1 : 0);
+            eloqstore::ChecksumBatch cb;
+            std::vector<uint8_t> ok;
+            while (Clock::now() < stop) {
+                Req r = make_req(pool, t, rng, max_n);
+                char* bad = const_cast<char*>(r.ptrs[r.k]);
+                bad[r.byte] ^= 0x10;
+                size_t fb;
+                const uint8_t* v;
+                if (async) {
+                    cb.SubmitValidate(r.ptrs, P);
+                    while (!cb.Poll()) {
+                    }
+                    fb = cb.FirstBad();
+                    v = cb.Verdicts();
+                } else {
+                    ok.assign(r.ptrs.size(), 9);
+                    fb = eloqstore::ValidateChecksums(r.ptrs, P, ok.data());
+                    v = ok.data();
+                }
+                bad[r.byte] ^= 0x10;
+                bool good = fb == r.k;
+                for (size_t i = 0; i < r.ptrs.size(); ++i) good &= v[i] == (i != r.k);
+                if (!good) {
+                    if (errors.fetch_add(1) < 5)
+                        std::fprintf(stderr, "thread %d: n %zu slot %zu got first_bad %zu\n", t, r.ptrs.size(), r.k, fb);
+                }
+                calls.fetch_add(1, std::memory_order_relaxed);
+            }
+        });
+    for (auto& x : th) x.join();
+    return errors.load();
+}
+}  // namespace
+
+int main() {
+    constexpr int T = 8;
+    const size_t np = T * PER;
+    char* pool = static_cast<char*>(std::aligned_alloc(4096, np * P));
+    CHECK(pool);
+    oracle_fill_pages(pool, P, np, 0x7E57, 0);
+    for (size_t i = 0; i < np; ++i) oracle_set_checksum(pool + i * P, P);
+    eloqstore::RegisterPagePool(pool, np * P);
+    eloqstore::StartChecksumService(4, 1000);
+
+    // 1 + 2: exact verdicts under eight native threads, gate off
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 0) == PCS_OK);
+    for (int async = 0; async < 2; ++async) {
+        std::atomic<uint64_t> calls{0};
+        const Counts c0 = counts();
+        CHECK(run_validate(pool, T, 0.5, async, 48, calls) == 0);
+        const Counts c1 = counts();
+        const uint64_t served = c1.served - c0.served, launched = c1.launched - c0.launched;
+        CHECK(served + launched == calls.load() && served > 0);
+        std::printf("%s validate, %d threads, gate off: %llu requests exact (%llu served, %llu launched)\n",
+                    async ? "async" : "sync", T, (unsigned long long)calls.load(), (unsigned long long)served,
+                    (unsigned long long)launched);
+    }
+
+    // 3: stamps of disjoint pages from eight threads
+    {
+        std::vector<uint8_t> named(np, 0);
+        for (size_t i = 0; i < np; ++i) std::memset(pool + i * P, 0, 8);
+        std::vector<std::thread> th;
+        const Counts c0 = counts();
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                uint64_t rng = 0x57A0ull + t;
+                for (int it = 0; it < 200; ++it) {
+                    const size_t n = 1 + splitmix(rng) % 24;
+                    std::vector<char*> ptrs;
+                    for (size_t i = 0; i < n; ++i) {
+                        const size_t p = splitmix(rng) % (PER - 16);  // the last 16 of each range stay unnamed
+                        bool dup = false;
+                        for (char* q : ptrs) dup |= q == pool + (t * PER + p) * P;
+                        if (dup) continue;
+                        ptrs.push_back(pool + (t * PER + p) * P);
+                        named[t * PER + p] = 1;
+                    }
+                    eloqstore::SetChecksums(ptrs, P);
+                }
+            });
+        for (auto& x : th) x.join();
+        const Counts c1 = counts();
+        for (size_t i = 0; i < np; ++i) {
+            uint64_t hdr;
+            std::memcpy(&hdr, pool + i * P, 8);
+            CHECK(named[i] ? hdr == oracle_page_xxh3(pool + i * P, P) : hdr == 0);
+        }
+        for (size_t i = 0; i < np; ++i) oracle_set_checksum(pool + i * P, P);
+        std::printf("stamps, %d threads: headers exact (%llu served, %llu launched)\n", T,
+                    (unsigned long long)(c1.served - c0.served), (unsigned long long)(c1.launched - c0.launched));
+    }
+
+    // 4: the contention gate at its default
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
+    for (int threads : {1, 8}) {
+        std::atomic<uint64_t> calls{0};
+        run_validate(pool, threads, 0.1, false, 6, calls);  // settle the average
+        calls = 0;
+        const Counts c0 = counts();
+        CHECK(run_validate(pool, threads, 0.4, false, 6, calls) == 0);
+        const Counts c1 = counts();
+        const double share = (double)(c1.served - c0.served) / (double)calls.load();
+        std::printf("gate 2, %d threads: %llu requests, served share %.3f\n", threads,
+                    (unsigned long long)calls.load(), share);
+        CHECK(threads == 1 ? share == 1.0 : share < 0.2);
+    }
+
+    eloqstore::StopChecksumService();
+    eloqstore::UnregisterPagePool(pool);
+    std::free(pool);
+    std::printf("service threads ok\n");
+    return 0;
+}

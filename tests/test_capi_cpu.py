@@ -29,15 +29,69 @@ def test_library_exports_every_header_symbol():
     assert set(funcs) == set(pcs._SIGS)
 
 
+SINGLE_PAGE = ("eloqstore::SetChecksum(std::basic_string_view<char, std::char_traits<char> >)",
+               "eloqstore::ValidateChecksum(std::basic_string_view<char, std::char_traits<char> >)")
+
+
+def _exports(path):
+    return subprocess.run(["nm", "-D", "-C", "--defined-only", path], capture_output=True, text=True,
+                          check=True).stdout
+
+
 def test_cpp_dropin_symbols_exported():
-    out = subprocess.run(["nm", "-D", "-C", "--defined-only", pcs.LIB_PATH], capture_output=True, text=True,
-                         check=True).stdout
-    for sym in ("eloqstore::SetChecksum(std::basic_string_view<char, std::char_traits<char> >)",
-                "eloqstore::ValidateChecksum(std::basic_string_view<char, std::char_traits<char> >)",
-                "eloqstore::ValidateChecksums(", "eloqstore::SetChecksums(", "eloqstore::PageDigests(",
-                "eloqstore::ChecksumBatch::Poll()", "eloqstore::ManifestChecksum(", "eloqstore::ValidateManifestRecord(",
-                "eloqstore::RegisterPagePool(", "eloqstore::UnregisterPagePool("):
+    """The batch library exports the batched C++ forms but NOT page.h's two
+    single-page names (include/storage/page.h:25-26): those live only in the
+    opt-in libeloqstore_pcs_dropin.so, so linking the batch library can never
+    interpose on page.cpp's definitions, whatever the link or DSO order."""
+    out = _exports(pcs.LIB_PATH)
+    for sym in ("eloqstore::ValidateChecksums(", "eloqstore::SetChecksums(", "eloqstore::PageDigests(",
+                "eloqstore::TryValidateChecksums(", "eloqstore::TrySetChecksums(", "eloqstore::LastChecksumError()",
+                "eloqstore::ChecksumBatch::Poll()", "eloqstore::ChecksumBatch::TryPoll()",
+                "eloqstore::ChecksumBatch::TrySubmitValidate(", "eloqstore::ManifestChecksum(",
+                "eloqstore::ValidateManifestRecord(", "eloqstore::RegisterPagePool(", "eloqstore::UnregisterPagePool("):
         assert sym in out, sym
+    for sym in SINGLE_PAGE:
+        assert sym not in out, sym
+    drop = _exports(pcs.DROPIN_LIB_PATH)
+    for sym in SINGLE_PAGE:
+        assert sym in drop, sym
+    assert "eloqstore::ValidateChecksums(" not in drop
+
+
+@pytest.mark.parametrize("order", ["ref_first", "pcs_first"])
+def test_single_page_calls_resolve_to_page_cpp_in_any_link_order(order):
+    """A shared object defining page.cpp's SetChecksum / ValidateChecksum
+    (tests/cpp/ref_page_stub.cpp, as an EloqStore embedded as a DSO would
+    carry them) linked beside the batch library in both orders: every
+    single-page call reaches it (its call counter), and without a GPU the
+    non-aborting batch form reports PCS_ERR_NO_DEVICE instead of aborting.
+    The GPU half (tests/test_gpu_parity.py) runs the batched API beside it."""
+    exe = os.path.join(os.path.dirname(__file__), "cpp", f"linkorder_{order}")
+    args = [exe] + (["--gpu"] if HAVE_GPU else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "linkorder ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_fail_inject_knob_fails_host_batches_loudly():
+    """PCS_TUNE_FAIL_INJECT (test only): the next k host-batch calls fail with
+    PCS_ERR_HIP before touching the GPU, so call sites can prove their
+    fallback to the reference loop."""
+    so = pcs.lib()
+    pages = [bytearray(4096) for _ in range(3)]
+    arr, _keep = pcs._page_ptrs(pages)
+    okb = (ctypes.c_uint8 * 3)()
+    fbv = ctypes.c_uint64()
+    try:
+        pcs.set_tuning(pcs.TUNE_FAIL_INJECT, 2)
+        assert pcs.get_tuning(pcs.TUNE_FAIL_INJECT) == 2
+        assert so.pcs_pages_validate_host(arr, 4096, 3, 0, okb, ctypes.byref(fbv)) == pcs.PCS_ERR_HIP
+        assert b"injected failure" in so.pcs_last_error()
+        assert so.pcs_pages_stamp_host(arr, 4096, 3, 0) == pcs.PCS_ERR_HIP
+        assert pcs.get_tuning(pcs.TUNE_FAIL_INJECT) == 0
+        # skip_verify computes nothing, so it never fails
+        assert so.pcs_pages_validate_host_ex(arr, 4096, 3, 0, okb, ctypes.byref(fbv), 1) == pcs.PCS_OK
+    finally:
+        pcs.set_tuning(pcs.TUNE_FAIL_INJECT, 0)
 
 
 def test_version_string():
@@ -119,6 +173,10 @@ def test_counters_and_tuning_defaults():
     assert pcs.get_tuning(5) == -1  # retired (in-place stamp width)
     assert pcs.get_tuning(pcs.TUNE_XXH3_SPLIT_PAGES) == 8192
     assert pcs.get_tuning(pcs.TUNE_INLINE_LIST) == 1
+    assert pcs.get_tuning(pcs.TUNE_SERVICE_MAX_CALLERS) == 2
+    assert pcs.get_tuning(pcs.TUNE_SERVICE_TEAR_TEST) == 0
+    assert pcs.get_tuning(pcs.TUNE_FAIL_INJECT) == 0
+    assert pcs.lib().pcs_counter(pcs.COUNTER_SERVICE_TORN_REQUESTS) == 0
 
 
 def test_skip_verify_flag_needs_no_gpu():

@@ -11,7 +11,12 @@ batch on the GPU, a 6-page scan-prefetch batch (types.h:31) and a 10-page
 write tail on page.cpp's CPU loop, told apart by call counters and
 pcs_counter().  Manifest records below and above kGpuManifestMinBytes go
 through Finalize, ValidateChecksum and the replay check (replayer.cpp:92),
-with a flipped byte rejected."""
+with a flipped byte rejected.  With the validate service on, the async
+snippet and straight ChecksumBatch batches (6 and 32 pages, stamps) are
+served by it, and a service stopped under an in-flight batch re-runs it on
+the launch path.  An injected GPU failure (PCS_TUNE_FAIL_INJECT) makes the
+sync and async read snippets and the flush snippet fall back to page.cpp's
+loop, which still finds the corrupted page."""
 import os
 import subprocess
 
@@ -33,6 +38,10 @@ def test_integration_snippets_run():
     assert "write path append=1: 10 pages stamped (reference loop)" in r.stdout
     assert "write path append=0: 40 pages stamped (reference loop)" in r.stdout
     assert "6-page scan batch on the reference loop" in r.stdout
-    assert "read path with the validate service: ok (32 and 128 pages served, 6 on the reference loop)" in r.stdout
+    assert "read path with the validate service: ok (32 and 128 pages served, 6 on the reference loop" in r.stdout
+    assert "async batch of 6 pages through the service: ok" in r.stdout
+    assert "async batch of 32 pages through the service: ok" in r.stdout
+    assert "stop during an async batch re-runs it" in r.stdout
+    assert "GPU failure fallback: ok" in r.stdout
     assert r.stdout.count("manifest record") == 2
     assert "(reference loop)" in r.stdout.split("manifest record")[1] and "(GPU)" in r.stdout.split("manifest record")[2]

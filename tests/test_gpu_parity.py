@@ -645,7 +645,18 @@ def test_cpp_dropin_program():
     assert r.returncode == 0 and "dropin ok" in r.stdout, r.stdout + r.stderr
 
 
-ANY_SIZES = [249, 250, 255, 257, 1000, 1032, 1033, 1039, 1040, 1096, 2047, 2049, 4000, 4095, 4097, 4104, 4160, 5000,
+@pytest.mark.parametrize("order", ["ref_first", "pcs_first"])
+def test_batch_api_beside_page_cpp_in_any_link_order(order):
+    """page.cpp's single-page functions in a shared object beside the batch
+    library, both link orders: single-page calls reach page.cpp (call
+    counter), the batched validate / stamp run on the GPU and match the
+    oracle, and never call page.cpp's functions (tests/cpp/linkorder_test.cpp)."""
+    exe = os.path.join(os.path.dirname(__file__), "cpp", f"linkorder_{order}")
+    r = subprocess.run([exe, "--gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "linkorder ok (gpu)" in r.stdout, r.stdout + r.stderr
+
+
+ANY_SIZES =[249, 250, 255, 257, 1000, 1032, 1033, 1039, 1040, 1096, 2047, 2049, 4000, 4095, 4097, 4104, 4160, 5000,
              8000, 12345, 16000, 65535]
 
 

@@ -126,35 +126,228 @@ def test_service_declines_what_it_cannot_serve(service):
     assert ok == [1] * 8 and fb is None and pcs.counter(SVC) == s0
 
 
-def test_service_under_threads(service):
-    """Four threads validating at once: one request at a time goes through
-    the service, a call that finds it busy takes the launch path; each thread
-    gets its own batch's verdicts either way."""
-    P = 4096
-    with stamped_pool(1024, P, 0x5EB) as pool:
+@pytest.fixture
+def no_gate():
+    """The contention gate off (PCS_TUNE_SERVICE_MAX_CALLERS = 0), so
+    concurrent callers still reach the service's one request line."""
+    pcs.set_tuning(pcs.TUNE_SERVICE_MAX_CALLERS, 0)
+    try:
+        yield
+    finally:
+        pcs.set_tuning(pcs.TUNE_SERVICE_MAX_CALLERS, 2)
+
+
+def test_service_under_threads(service, no_gate):
+    """Four threads validating at once, every request carrying a corrupted
+    page of its own at a random slot (low slots included: those addresses
+    come with the polled request words): one request at a time goes through
+    the service, a call that finds it busy takes the launch path, and each
+    thread gets exactly its own batch's verdicts and first_bad.  A request
+    served with another request's page addresses would report the wrong
+    slot (or none)."""
+    P, T, per = 4096, 4, 256
+    with stamped_pool(T * per, P, 0x5EB) as pool:
         errors = []
 
         def worker(t):
             rng = np.random.default_rng(100 + t)
             try:
-                for _ in range(60):
+                for _ in range(80):
                     n = int(rng.integers(1, 64))
-                    idx = rng.permutation(1024)[:n]
+                    idx = t * per + rng.permutation(per)[:n]
+                    k = int(rng.integers(0, min(n, 14))) if rng.random() < 0.7 else int(rng.integers(0, n))
+                    pool.pages[idx[k], 8 + int(rng.integers(0, P - 8))] ^= 0x10
                     ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
-                    if not (ok.all() and fb is None):
-                        errors.append((t, n, fb))
+                    want = np.ones(n, dtype=bool)
+                    want[k] = False
+                    if fb != k or not np.array_equal(ok.astype(bool), want):
+                        errors.append((t, n, k, fb))
+                    pcs.stamp_ptrs(pool.ptr(idx[k:k + 1]), P)  # heal: restamp the flipped page
             except Exception as e:  # noqa: BLE001
                 errors.append((t, repr(e)))
 
         s0, z0 = counters()
-        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
         for x in th:
             x.start()
         for x in th:
             x.join()
-        assert not errors
+        assert not errors, errors[:5]
         s1, z1 = counters()
-        assert s1 - s0 + z1 - z0 == 240 and s1 > s0
+        assert s1 - s0 + z1 - z0 == 2 * T * 80 and s1 > s0
+
+
+def test_service_alternating_page_sets(service):
+    """Back-to-back requests from one thread whose page sets alternate
+    (A, B, A, ...) in the polled slots 0-11 and beyond, with a corrupted page
+    in a low slot on every other request: every request's verdicts belong
+    to its own pages (a poll pairing the new seq with the previous request's
+    addresses would validate the wrong set)."""
+    P = 4096
+    with stamped_pool(512, P, 0x5F0) as pool:
+        rng = np.random.default_rng(7)
+        s0, _ = counters()
+        calls = 0
+        for n in (5, 12, 13, 40):
+            sets = [rng.permutation(256)[:n], 256 + rng.permutation(256)[:n]]
+            for i in range(60):
+                idx = sets[i % 2]
+                k = None
+                if i % 4 in (1, 2):
+                    k = (i // 4) % min(n, 12)
+                    pool.pages[idx[k], 777] ^= 0x02
+                ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                calls += 1
+                want = np.ones(n, dtype=bool)
+                if k is not None:
+                    want[k] = False
+                    pool.pages[idx[k], 777] ^= 0x02
+                assert fb == k and np.array_equal(ok.astype(bool), want), (n, i, k, fb)
+        assert pcs.counter(SVC) == s0 + calls
+
+
+def test_service_torn_line_drill(service):
+    """PCS_TUNE_SERVICE_TEAR_TEST posts seq first and writes the request
+    words 30 us later, so the waiting kernel's polls see the new seq beside
+    the previous request's page addresses and count.  The check word must
+    make the kernel ignore every such poll: verdicts stay exact for
+    alternating page sets, and the kernel reports the torn lines it saw
+    (PCS_COUNTER_SERVICE_TORN_REQUESTS)."""
+    P = 4096
+    with stamped_pool(256, P, 0x5F1) as pool:
+        sets = [np.arange(0, 6), np.arange(100, 110)]
+        torn0 = pcs.counter(pcs.COUNTER_SERVICE_TORN_REQUESTS)
+        s0, _ = counters()
+        pcs.set_tuning(pcs.TUNE_SERVICE_TEAR_TEST, 30)
+        try:
+            for i in range(40):
+                idx = sets[i % 2]
+                k = i % len(idx) if i % 2 else None
+                if k is not None:
+                    pool.pages[idx[k], 9] ^= 0x80
+                ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                want = np.ones(len(idx), dtype=bool)
+                if k is not None:
+                    want[k] = False
+                    pool.pages[idx[k], 9] ^= 0x80
+                assert fb == k and np.array_equal(ok.astype(bool), want), (i, k, fb)
+        finally:
+            pcs.set_tuning(pcs.TUNE_SERVICE_TEAR_TEST, 0)
+        assert pcs.counter(SVC) == s0 + 40
+        torn = pcs.counter(pcs.COUNTER_SERVICE_TORN_REQUESTS) - torn0
+        assert torn >= 20, torn  # most requests found a waiting kernel polling through the gap
+
+
+def test_service_stamps_under_threads(service, no_gate):
+    """Stamps from four threads on disjoint pages, served by the service or
+    the launch path: every stamped header matches the oracle and the pages
+    no request named keep their zero header."""
+    P, T, per = 4096, 4, 128
+    with pcs.PagePool(T * per, P) as pool:
+        pool.pages[:] = oracle.fill_pages(P, T * per, 0x5F2).reshape(T * per, P)
+        pool.pages[:, :8] = 0
+        want = oracle.pages_digest(pool.pages.reshape(-1), P, 0)
+        named = np.zeros(T * per, dtype=bool)
+        errors = []
+
+        def worker(t):
+            rng = np.random.default_rng(300 + t)
+            try:
+                for _ in range(40):
+                    n = int(rng.integers(1, 24))
+                    idx = t * per + rng.permutation(per - 8)[:n]  # the last 8 pages of each range stay unnamed
+                    named[idx] = True
+                    pcs.stamp_ptrs(pool.ptr(idx), P)
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        s0, _ = counters()
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:5]
+        hdr = pool.pages[:, :8].copy().view(np.uint64).ravel()
+        assert np.array_equal(hdr[named], want[named])
+        assert not hdr[~named].any()
+        assert pcs.counter(SVC) > s0
+
+
+def test_service_native_threads_and_gate():
+    """tests/cpp/service_threads_test.cpp: eight native threads (Python
+    threads serialise on the GIL between calls and never keep eight calls in
+    flight): sync and async validates with a corrupted page of their own in
+    every request, exact verdicts and first_bad on either path; stamps of
+    disjoint pages against the oracle; the contention gate at its default
+    serving every call of one thread and declining nearly all of eight."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "service_threads_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "service threads ok" in r.stdout, r.stdout + r.stderr
+    print(r.stdout)
+
+
+def test_service_async_batches(service):
+    """ChecksumBatch (pcs_batch_*) validate and stamp batches posted to the
+    service: submit returns at once, poll watches the verdict words;
+    verdicts, first_bad and stamped headers against the oracle; the service
+    counter shows they were served and no launch happened."""
+    P = 4096
+    with stamped_pool(512, P, 0x5F4) as pool:
+        b = pcs.Batch()
+        try:
+            for n, k in ((6, 4), (32, 0), (128, 100), (256, 255)):
+                idx = np.random.default_rng(n).permutation(512)[:n]
+                pool.pages[idx[k], 3000] ^= 0x40
+                s0, z0 = counters()
+                b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(idx), P)
+                polls = 0
+                while not b.poll():
+                    polls += 1
+                ok, fb = b.result()
+                pool.pages[idx[k], 3000] ^= 0x40
+                assert fb == k and sum(ok) == n - 1 and ok[k] == 0, (n, fb)
+                assert counters() == (s0 + 1, z0), n
+            idx = np.arange(300, 340)
+            pool.pages[idx, :8] = 0
+            s0, z0 = counters()
+            b.submit_ptrs(pcs.Batch.STAMP, pool.ptr(idx), P)
+            b.wait()
+            assert counters() == (s0 + 1, z0)
+            want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0)
+            assert np.array_equal(pool.pages[idx, :8].copy().view(np.uint64).ravel(), want)
+            assert b.result() == [int(x) for x in want]
+        finally:
+            b.close()
+
+
+def test_service_stop_with_async_batch_in_flight():
+    """Stopping the service while an asynchronous batch is posted to it: the
+    batch notices the service is gone and re-runs its pages on the launch
+    path by itself (exact verdicts); a restarted service serves again."""
+    P = 4096
+    with stamped_pool(256, P, 0x5F5) as pool:
+        idx = np.arange(10, 50)
+        pool.pages[idx[17], 64] ^= 0x08
+        b = pcs.Batch()
+        try:
+            for _ in range(6):
+                pcs._call("pcs_service_start", 4, 1000)
+                b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(idx), P)
+                pcs._call("pcs_service_stop")
+                b.wait()
+                ok, fb = b.result()
+                assert fb == 17 and sum(ok) == len(idx) - 1
+            pcs._call("pcs_service_start", 4, 1000)
+            s0, _ = counters()
+            b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(idx), P)
+            b.wait()
+            assert b.result()[1] == 17 and pcs.counter(SVC) == s0 + 1
+        finally:
+            b.close()
+            pcs._call("pcs_service_stop")
 
 
 def test_resident_kernel_does_not_hold_up_device_sync(service):
@@ -247,7 +440,7 @@ def test_service_left_running_at_exit():
     assert time.perf_counter() - t0 < 60
 
 
-def test_service_toggled_under_threads():
+def test_service_toggled_under_threads(no_gate):
     """Start and stop the service 20 times while four threads keep
     validating: every call lands on the service or the launch path with the
     oracle's verdicts (one corrupted page per batch), none hangs."""

@@ -73,17 +73,17 @@ int main() {
             zp[i] = static_cast<uint8_t*>(pool) + perm[i] * P;
             gp[i] = static_cast<uint8_t*>(loose) + perm[i] * P;
         }
-        const double z = median_us([&] { pcs_pages_validate_host(zp.data(), P, nb, PCS_XXH3_64, ok.data(), &fb, PCS_FLAG_NONE); });
-        const double g = median_us([&] { pcs_pages_validate_host(gp.data(), P, nb, PCS_XXH3_64, ok.data(), &fb, PCS_FLAG_NONE); });
+        const double z = median_us([&] { pcs_pages_validate_host(zp.data(), P, nb, PCS_XXH3_64, ok.data(), &fb); });
+        const double g = median_us([&] { pcs_pages_validate_host(gp.data(), P, nb, PCS_XXH3_64, ok.data(), &fb); });
         pcs_batch* b;
         pcs_batch_create(&b);
         const double a = median_us([&] {
-            pcs_batch_submit(b, PCS_BATCH_VALIDATE, zp.data(), P, nb, PCS_XXH3_64, PCS_FLAG_NONE);
+            pcs_batch_submit(b, PCS_BATCH_VALIDATE, zp.data(), P, nb, PCS_XXH3_64);
             while (pcs_batch_poll(b) == 0) {
             }
         });
         const double sub = median_us([&] {
-            pcs_batch_submit(b, PCS_BATCH_VALIDATE, zp.data(), P, nb, PCS_XXH3_64, PCS_FLAG_NONE);
+            pcs_batch_submit(b, PCS_BATCH_VALIDATE, zp.data(), P, nb, PCS_XXH3_64);
             pcs_batch_wait(b);
         });
         pcs_batch_destroy(b);
