@@ -20,8 +20,10 @@ only the CPU reference over the 1 GiB file (BASELINE configs[0]).
 Also reported, on the same line:
   roofline      dominant kernel's algorithmic bytes per launch / average launch
                 time (HIP events on the launch stream) vs 8 TB/s HBM peak;
-                traffic = PMC-measured HBM bytes per launch from the committed
-                rocprofv3 summary under profiles/ (else null).
+                traffic = PMC-measured HBM bytes per launch: at the default
+                config, two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
+                over the headline kernel in this run (traffic_live); else, or
+                if those fail, the committed summary under profiles/.
   stream_read   the fastest plain streaming read of the same buffer we could
                 write (pcs_stream_read_dev, no hash): the practical read rate
                 of the part, within ~1 % of the hash kernels on 4 KiB pages
@@ -30,8 +32,11 @@ Also reported, on the same line:
   cpu_baseline  BASELINE config 1: the reference's own xxHash (oracle/_ref) on
                 ONE host thread, reading every page of a 1 GiB file of 4 KiB
                 pages and validating it like page_checksum_tool / page.cpp:25-31;
-                cpu_all_cores: the same over all usable host cores; cli_scan:
-                this repo's GPU CLI (--scan) over the same file.
+                cpu_all_cores: the same over all usable host cores;
+                cpu_ref_inmem: the reference's xxhash.c over the same pages
+                already in memory, one thread (no pread per page); cpu_port:
+                the repo's C restatement likewise; cli_scan: this repo's GPU
+                CLI (--scan) over the same file.
   parity        sampled GPU digests (every 4096th page, first/last 64) against
                 the reference xxHash on the host.
   sweep         (N=1) every other BASELINE config and mode, one entry each:
@@ -411,10 +416,25 @@ def config1(target_s: float, all_cores_s: float | None, workdir: str | None = No
                 "sample": f"config 1 file in memory, {reps} passes of oracle/xxh_oracle.c (the repo's C restatement, "
                           f"gcc -O2) per page, one thread",
                 "pages_failed": int((got != want).sum())}
+        # The reference's own xxhash.c over the same pages already in memory
+        # (no pread per page): the in-memory anchor beside the pread-bound
+        # cpu_baseline, one thread
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            got = oracle.ref_pages_digest(data, P, 0)
+            reps += 1
+            if time.perf_counter() - t0 >= min(5.0, target_s):
+                break
+        dt = time.perf_counter() - t0
+        inmem = {"value": round(reps * n * P / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "reference",
+                 "sample": f"config 1 file in memory (one 1 GiB buffer), {reps} passes of the reference's "
+                           f"external/xxhash.c v0.8.3 XXH3_64bits over [8, 4096) of every page (gcc -O2, SSE2, "
+                           f"oracle/_ref), one thread",
+                 "pages_failed": int((got != want).sum())}
         del data
         r = subprocess.run([pcs.TOOL_PATH, "--scan", path, str(P)], capture_output=True, text=True, timeout=300)
         scan = {"rc": r.returncode, "line": r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr.strip()}
-        return {"cpu_baseline": one, "cpu_all_cores": allc, "cpu_port": port, "cli_scan": scan}
+        return {"cpu_baseline": one, "cpu_all_cores": allc, "cpu_port": port, "cpu_ref_inmem": inmem, "cli_scan": scan}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -659,6 +679,68 @@ def committed_traffic(cfg: int, algo: int):
     return best
 
 
+LIVE_KERNEL = "pcs::k_xxh3_fixed<4096, 0, "  # the headline's dominant kernel (config 2, XXH3 digest)
+
+
+def pmc_child() -> None:
+    """--pmc-child: the headline workload's kernel, 4 launches, nothing else
+    timed; run under rocprofv3 --pmc by live_traffic()."""
+    torch.cuda.set_device(0)
+    w = Workload(2, pcs.XXH3_64, 0, None, "cuda:0")
+    for _ in range(4):
+        w.step("digest")
+    torch.cuda.synchronize()
+    print("pmc child ok", flush=True)
+
+
+def live_traffic(timeout_s: int = 90):
+    """roofline.traffic measured on THIS box in THIS run: rocprofv3 --pmc
+    FETCH_SIZE and --pmc WRITE_SIZE in separate passes (their TCC counters do
+    not fit one pass on gfx950) over a child process running the headline
+    kernel (bench.py --pmc-child), corrected as MI355X_MICROARCH.md's HBM
+    section prescribes for gfx950: read = FETCH_SIZE (KiB) * 1024 * 2 (it
+    counts half the bytes of a wide streaming read), write = WRITE_SIZE (KiB) *
+    1024; median over the kernel's dispatches.  Each pass runs under
+    `timeout -s KILL` (a --pmc run that asks for more counters than the
+    hardware has hangs)."""
+    import csv
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    per = {}
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="pcs_pmc_")
+        try:
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", counter, "-d", d, "-o", counter.lower(),
+                   "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--pmc-child"]
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s + 30, env=env, cwd=ROOT)
+            if r.returncode != 0 or "pmc child ok" not in r.stdout:
+                raise RuntimeError(f"rocprofv3 --pmc {counter}: rc {r.returncode}: {(r.stderr or r.stdout)[-300:]}")
+            vals = []
+            for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(path) as f:
+                    for row in csv.DictReader(f):
+                        if LIVE_KERNEL in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                raise RuntimeError(f"rocprofv3 --pmc {counter}: no dispatch of {LIVE_KERNEL}")
+            per[counter] = (statistics.median(vals), len(vals))
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    rd = per["FETCH_SIZE"][0] * 1024 * 2
+    wr = per["WRITE_SIZE"][0] * 1024
+    return {"traffic": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
+            "dispatches": {k: v[1] for k, v in per.items()},
+            "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --pmc-child in this run "
+                      "(read = FETCH_SIZE*1024*2, write = WRITE_SIZE*1024, median over dispatches)"}
+
+
 def guarded(name: str, fn, *a, **kw):
     """fn(*a, **kw), or {"error": ...} if it raises (the traceback goes to
     stderr): an optional leg never takes the headline line down with it."""
@@ -692,10 +774,17 @@ def main():
                     help="divide every sweep workload's page count (tests only; default 1 = the BASELINE sizes)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the host-memory path (pinned direct DMA and pageable gather)")
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="take roofline.traffic from the committed profiles/ summary instead of two rocprofv3 "
+                         "--pmc passes in this run")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--wall-budget", type=float, default=360.0,
                     help="seconds from start after which the optional legs (config 1, host-inclusive, "
                          "sweep entries) are skipped and recorded as such; the headline line always prints")
     args = ap.parse_args()
+    if args.pmc_child:
+        pmc_child()
+        return
     t_start = time.perf_counter()
     deadline = t_start + args.wall_budget
 
@@ -818,9 +907,17 @@ def main():
         else:
             c1 = guarded("config1", config1, args.cpu_seconds, all_s)
 
+    live = None
+    if (rank == 0 and world == 1 and cfg == 2 and algo == pcs.XXH3_64 and args.mode == "digest"
+            and args.pages_per_gpu is None and not args.no_live_traffic):
+        live = guarded("live_traffic", live_traffic) if time.perf_counter() + 60 < deadline else \
+            {"skipped": "bench wall budget spent"}
+
     if rank == 0:
         achieved = w.algorithmic_bytes(args.mode) / avg_launch / 1e9
         traffic = committed_traffic(cfg, algo) if args.mode == "digest" else None
+        if live and live.get("traffic"):
+            traffic = (live["traffic"], live["source"])
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -856,6 +953,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
+                "traffic_live": live,
                 "algorithmic_bytes_per_launch": w.algorithmic_bytes(args.mode),
                 "avg_launch_ms": round(avg_launch * 1e3, 4),
                 "launch_timing": f"HIP events bracketing the {args.steps} timed steps on the launch stream",
@@ -866,7 +964,7 @@ def main():
         }
         line["corruption_drill"] = drill
         if c1 is not None:
-            for k in ("cpu_all_cores", "cpu_port", "cli_scan"):
+            for k in ("cpu_all_cores", "cpu_port", "cpu_ref_inmem", "cli_scan"):
                 line[k] = c1.get(k)
             for k in ("error", "skipped"):
                 if k in c1:

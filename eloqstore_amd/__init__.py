@@ -82,6 +82,7 @@ _SIGS = {
     "pcs_service_stop": [],
     "pcs_service_running": [],
     "pcs_version": [],
+    "pcs_abi_version": [],
     "pcs_last_error": [],
 }
 _STR = {"pcs_version", "pcs_last_error"}
@@ -183,6 +184,13 @@ def get_tuning(key: int) -> int:
 
 def version() -> str:
     return lib().pcs_version().decode()
+
+
+ABI_VERSION = 4  # PCS_ABI_VERSION of include/eloqstore_pcs.h this binding was written for
+
+
+def abi_version() -> int:
+    return int(lib().pcs_abi_version())
 
 
 def device_count() -> int:

@@ -1066,7 +1066,9 @@ int batch_service_poll(pcs_batch* b) {
 
 extern "C" {
 
-const char* pcs_version(void) { return "eloqstore-pcs 0.3.0 (gfx950; xxHash v0.8.3 page path)"; }
+const char* pcs_version(void) { return "eloqstore-pcs 0.4.0 (gfx950; xxHash v0.8.3 page path)"; }
+
+int pcs_abi_version(void) { return PCS_ABI_VERSION; }
 
 const char* pcs_last_error(void) { return t_last_error.c_str(); }
 

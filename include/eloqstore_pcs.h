@@ -78,7 +78,19 @@ enum pcs_flags {
     PCS_FLAG_SKIP_VERIFY = 1u << 0,
 };
 
-/* ---- library / device ---------------------------------------------------- */
+/* ---- library / device ----------------------------------------------------
+ * ABI version of this header.  Compare pcs_abi_version() with PCS_ABI_VERSION
+ * once at start-up: a library built from another header revision then fails
+ * loudly instead of reading arguments it was not given.
+ *   3  round 3: pcs_pages_validate_host and pcs_batch_submit lost the trailing
+ *      flags word they had in round 2 (the flags moved to the _ex forms); a
+ *      caller built against the old prototypes links but its flags are
+ *      ignored, which pcs_abi_version() detects
+ *   4  round 4: PCS_TUNE_SERVICE_TEAR_TEST / FAIL_INJECT / SERVICE_MAX_CALLERS,
+ *      PCS_COUNTER_SERVICE_TORN_REQUESTS; the C++ single-page SetChecksum /
+ *      ValidateChecksum moved to libeloqstore_pcs_dropin.so */
+#define PCS_ABI_VERSION 4
+int pcs_abi_version(void);
 const char *pcs_version(void);
 const char *pcs_last_error(void);
 int pcs_device_count(int *count);

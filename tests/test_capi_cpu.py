@@ -98,6 +98,15 @@ def test_version_string():
     assert "gfx950" in pcs.version()
 
 
+def test_abi_version_matches_header():
+    """the library reports the header revision it was built
+    from; callers compare it with PCS_ABI_VERSION at start-up."""
+    import re
+    text = open(pcs.HEADER_PATH).read()
+    want = int(re.search(r"#define PCS_ABI_VERSION (\d+)", text).group(1))
+    assert pcs.abi_version() == want == pcs.ABI_VERSION
+
+
 @pytest.mark.skipif(HAVE_GPU, reason="checks the no-GPU failure path")
 def test_no_gpu_fails_loudly():
     so = pcs.lib()

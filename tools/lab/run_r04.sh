@@ -1,0 +1,14 @@
+# Round-4 full check on one box: GPU suite, smoke, default bench line (with
+# its live rocprofv3 --pmc traffic leg), then the rocprofv3 sweep.
+# usage: bash tools/lab/run_r04.sh <tag>
+set -o pipefail
+TAG=${1:-r04a}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 && \
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")" > "$OUT/smoke.log" 2>&1 && \
+timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && \
+bash tools/profile_sweep.sh "$TAG" > "$OUT/sweep.log" 2>&1
+rc=$?
+echo "rc=$rc"; tail -1 "$OUT/gpu_tests.log"
+exit $rc
