@@ -158,9 +158,9 @@ TUNE_MANIFEST_WIDE = 13
 TUNE_XXH64_WAVES = 15
 TUNE_ZC_POLL = 23
 TUNE_SERVICE_STREAM = 24
-TUNE_SERVICE_TEAR_TEST = 25  # test only
-TUNE_FAIL_INJECT = 26  # test only
-TUNE_SERVICE_MAX_CALLERS = 27
+TUNE_SERVICE_TEAR_TEST = 26  # test only
+TUNE_FAIL_INJECT = 27  # test only
+TUNE_SERVICE_MAX_CALLERS = 28
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -1403,7 +1403,7 @@ uint64_t next_call_id() {
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 28;
+constexpr int kTuneKeys = 29;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1414,10 +1414,11 @@ constexpr int kTuneKeys = 28;
 // 20 4 KiB-aligned descriptor steps (+-0.2 %, aligned_steps_lab.txt), 21 the
 // descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt);
 // round 3: 22 the XXH64 direct-to-LDS segment ring (config 3 -0.8..-34 %,
-// profiles/r03/x64_glds_ab_*.txt).  Setting one fails.
+// profiles/r03/x64_glds_ab_*.txt), 25 XXH64 tile-order chunks (no gain, a lab
+// knob in commit 01e849b).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, false, false, false};
+                                      false, true,  false, false, false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1434,6 +1435,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired (round 3: XXH64 direct-to-LDS ring)*/ 0,
                                           /*zero-copy validate: completion from the verdicts themselves*/ 1,
                                           /*validate service stream: 1 highest priority, 0 plain*/ 1,
+                                          /*retired (round 3 lab: XXH64 tile-order chunks)*/ 0,
                                           /*test only: validate service torn-line drill, microseconds*/ 0,
                                           /*test only: host-batch calls left to fail*/ 0,
                                           /*validate service contention gate: callers (0 = off)*/ 2};
@@ -1707,7 +1709,11 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, word, id);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
-            const unsigned ggrid = grid_for(n, kBlock, kBlocksPerCu);
+            // one block per CU: when every page conforms (the usual case)
+            // each block only reads the flag and leaves (a full-size grid
+            // took 4.3 us to do that, profiles/r04b_sweep.json); rare
+            // off-shape pages take the grid-stride loop
+            const unsigned ggrid = std::min(grid_for(n, kBlock, kBlocksPerCu), (unsigned)cu_count());
             hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(ggrid), dim3(kBlock), 0, s, base, off, len, n, algo, seed,
                                skip, 1, out, ok, fb, word, id);
             return hipGetLastError();

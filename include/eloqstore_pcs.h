@@ -303,11 +303,12 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     pcs_batch_poll / wait,
  *                                     pcs_manifest_*_host) fail with
  *                                     PCS_ERR_HIP; decremented per failure
- * Keys 4, 5, 10, 12, 14 and 16-22 selected variants that measured slower or no
+ * Keys 4, 5, 10, 12, 14, 16-22 and 25 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
  * tiles, plain result stores, 4 KiB-aligned descriptor steps, a 4-waves-
- * per-SIMD descriptor body; round 3: an XXH64 direct-to-LDS segment ring);
+ * per-SIMD descriptor body; round 3: an XXH64 direct-to-LDS segment ring,
+ * XXH64 tile-order chunks);
  * they were retired: setting one fails and reading one
  * returns -1. */
 enum pcs_tune_key {
@@ -323,9 +324,9 @@ enum pcs_tune_key {
     PCS_TUNE_XXH64_WAVES = 15,
     PCS_TUNE_ZC_POLL = 23,
     PCS_TUNE_SERVICE_STREAM = 24,
-    PCS_TUNE_SERVICE_TEAR_TEST = 25,
-    PCS_TUNE_FAIL_INJECT = 26,
-    PCS_TUNE_SERVICE_MAX_CALLERS = 27,
+    PCS_TUNE_SERVICE_TEAR_TEST = 26,
+    PCS_TUNE_FAIL_INJECT = 27,
+    PCS_TUNE_SERVICE_MAX_CALLERS = 28,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
