@@ -811,3 +811,41 @@ def test_huge_pages(P, n, algo):
     pcs.flip_byte(buf, P, n, every=n, byte_offset=P - 1)
     ok, fb = pcs.pages_validate(buf, P, n, algo)
     assert list(ok.cpu().numpy()) == [0] + [1] * (n - 1) and int(u64(fb)[0]) == 0
+
+
+def test_xxh64_desc_sparse_offshape_pages():
+    """XXH64 descriptor batch of 100,000 line-shaped 4 KiB pages with three
+    off-shape pages (8-byte-aligned, lengths not a multiple of 64) at the
+    first, a middle and the last index: the LDS kernel flags the call, the
+    gated generic pass (one block per CU, grid-stride) picks exactly those
+    pages up; the same batch without them leaves the generic pass idle.
+    Digests against the oracle at the odd pages and a sample of the rest."""
+    n, P = 100_000, 4096
+    lens = np.full(n, P, dtype=np.uint32)
+    odd = [0, 51_234, n - 1]
+    lens[odd] = [4100, 1000, 4168]
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        if i in odd:
+            pos += 8  # 8-byte aligned only: off the line shape
+        offs[i] = pos
+        pos += int(lens[i])
+        pos = (pos + 15) // 16 * 16
+    host = np.random.default_rng(64).integers(0, 256, size=pos + 64, dtype=np.uint8)
+    base = torch.from_numpy(host).to(DEV)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+    got = u64(pcs.desc_digest(base, d_off, d_len, n, pcs.XXH64))
+    check = np.unique(np.concatenate([odd, np.arange(1, n, 997)]))
+    want = oracle.desc_digest(host, offs[check], lens[check], pcs.XXH64)
+    assert np.array_equal(got[check], want)
+    # all line-shaped: the generic pass must not touch anything
+    lens2 = np.full(n, P, dtype=np.uint32)
+    offs2 = (np.arange(n, dtype=np.uint64) * P)
+    d_off2 = torch.from_numpy(offs2.view(np.int64)).to(DEV)
+    d_len2 = torch.from_numpy(lens2.view(np.int32)).to(DEV)
+    base2 = base[: n * P]
+    got2 = u64(pcs.desc_digest(base2, d_off2, d_len2, n, pcs.XXH64))
+    want2 = oracle.desc_digest(host[: n * P], offs2[check], lens2[check], pcs.XXH64)
+    assert np.array_equal(got2[check], want2)
