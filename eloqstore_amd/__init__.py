@@ -79,6 +79,7 @@ _SIGS = {
     "pcs_get_tuning": [_i32],
     "pcs_counter": [_i32],
     "pcs_service_start": [_i32, _u32],
+    "pcs_service_start_ex": [_i32, _i32, _u32],
     "pcs_service_stop": [],
     "pcs_service_running": [],
     "pcs_version": [],
@@ -445,11 +446,11 @@ class ValidateService:
     open, validate_ptrs / validate_checksums batches of up to 256 registered
     XXH3 pages go to a resident kernel instead of a launch each."""
 
-    def __init__(self, workgroups: int = 4, idle_us: int = 1000):
-        self.workgroups, self.idle_us = workgroups, idle_us
+    def __init__(self, workgroups: int = 4, idle_us: int = 1000, lines: int = 1):
+        self.workgroups, self.idle_us, self.lines = workgroups, idle_us, lines
 
     def __enter__(self):
-        _call("pcs_service_start", self.workgroups, self.idle_us)
+        _call("pcs_service_start_ex", self.lines, self.workgroups, self.idle_us)
         return self
 
     def __exit__(self, *exc):

@@ -55,35 +55,44 @@ int64_t get_tuning(int key);
 hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s);
 
 // Pre-armed validate service (pcs_service_*): a mailbox in pinned host
-// memory, read by the waiting kernel through its device alias.  The first
-// kServiceLineWords words (two 64-byte lines) carry a whole small request:
-// seq = generation << 32 | count, page count, page size, a check word and the
-// first kServiceLinePtrs page addresses, so the poll that sees a new seq
-// brings in a request of up to 12 pages.  The host writes seq last.  The 16
-// words arrive as separate per-lane loads, so nothing makes them one
+// memory, read by the waiting kernel through its device alias.  It holds up
+// to kServiceMaxLines request lines, one per concurrent caller; line k is
+// served by workgroups [k * wpl, (k + 1) * wpl) of the kernel.  The first
+// kServiceLineWords words of a line (two 64-byte lines) carry a whole small
+// request: seq = generation << 32 | count, page count, page size, a check
+// word and the first kServiceLinePtrs page addresses, so the poll that sees a
+// new seq brings in a request of up to 12 pages.  The host writes seq last.
+// The 16 words arrive as separate per-lane loads, so nothing makes them one
 // snapshot: the check word (the sum of service_word_mix over the other 15
 // words, written by the host just before seq) is what proves that a poll saw
 // one request's words and not a new seq beside an older request's page
 // addresses.  A poll whose words do not add up to their check word is
 // ignored and the line is read again.  Verdicts are 32-bit words stored
-// system-scope.
+// system-scope.  `gen` names the newest generation: a kernel of an older one
+// leaves at its next poll.
 constexpr int kServiceMaxPages = 256;
+constexpr int kServiceMaxLines = 8;
 constexpr int kServiceLineWords = 16;
 constexpr int kServiceCheckWord = 3;
 constexpr int kServiceLinePtrs = kServiceLineWords - 4;
 constexpr uint32_t kServicePending = 0xA5A5A5A5u;
 constexpr uint64_t kServiceStamp = 1ull << 32;  // in the page-size word: a stamp request
-struct ServiceBox {
+struct ServiceLine {
     alignas(64) uint64_t seq;
     uint64_t n;
     uint64_t page_size;               // | kServiceStamp for a stamp request
     uint64_t check;                   // sum of service_word_mix(word i, i) over the other line words
     uint64_t ptrs[kServiceMaxPages];  // device-visible page addresses
-    alignas(64) uint64_t stop;        // host: 1 ends every waiting kernel
-    uint64_t torn_seq;                // kernel: the last seq it saw beside words that failed the check
     alignas(64) uint32_t ok[kServiceMaxPages];
+    alignas(64) uint64_t torn_seq;    // kernel: the last seq it saw beside words that failed the check
 };
-static_assert(offsetof(ServiceBox, ptrs) == 4 * sizeof(uint64_t), "line words: seq, n, page_size, check, ptrs");
+struct ServiceBox {
+    alignas(64) uint64_t stop;  // host: 1 ends every waiting kernel
+    uint64_t gen;               // host: the newest generation (written before its kernel is queued)
+    ServiceLine line[kServiceMaxLines];
+};
+static_assert(offsetof(ServiceLine, ptrs) == 4 * sizeof(uint64_t), "line words: seq, n, page_size, check, ptrs");
+static_assert(offsetof(ServiceBox, gen) == offsetof(ServiceBox, stop) + 8, "stop and gen are one poll's two words");
 // murmur3's 64-bit finaliser over (word, position): a word read from an older
 // request changes the sum by a pseudo-random 64-bit amount.
 __host__ __device__ inline uint64_t service_word_mix(uint64_t w, uint64_t i) {
@@ -95,10 +104,12 @@ __host__ __device__ inline uint64_t service_word_mix(uint64_t w, uint64_t i) {
     x ^= x >> 33;
     return x;
 }
-// Queue one service kernel of generation `gen`: it serves that generation's
-// requests until idle_ticks pass without one or, between requests, it has
-// lived life_ticks (both on the 100 MHz real-time clock), or stop is set.
-hipError_t run_service(ServiceBox* d_box, int workgroups, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+// Queue one service kernel of generation `gen`: lines * wpl workgroups,
+// workgroup w serving line w / wpl.  Each serves its line's requests of that
+// generation until idle_ticks pass without one or, between requests, it has
+// lived life_ticks (both on the 100 MHz real-time clock), or stop is set, or
+// the box names a newer generation.
+hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                        hipStream_t s);
 
 }  // namespace pcs

@@ -64,8 +64,8 @@ void UnregisterPagePool(void* base) {
     if (int rc = pcs_host_unregister(base)) die("UnregisterPagePool", rc);
 }
 
-void StartChecksumService(int workgroups, uint32_t idle_us) {
-    if (int rc = pcs_service_start(workgroups, idle_us)) die("StartChecksumService", rc);
+void StartChecksumService(int workgroups, uint32_t idle_us, int lines) {
+    if (int rc = pcs_service_start_ex(lines, workgroups, idle_us)) die("StartChecksumService", rc);
 }
 
 void StopChecksumService() {

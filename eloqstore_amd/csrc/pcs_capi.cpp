@@ -504,40 +504,57 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // pre-armed validate service (pcs_service_*)
 // ---------------------------------------------------------------------------
 // One service per device, started and stopped on the calling thread's current
-// device, and one request line per device.  A request (a synchronous
-// validate / stamp call, or an asynchronous pcs_batch) claims the line with
-// an atomic flag, writes the request words, posts seq, and is answered
-// through the verdict words; the flag is released when the owner has read
-// its results.  A call that finds the line owned takes the launch path
-// instead of queueing behind it, so threads never starve on the one line.
-// Requests are served by a resident kernel (pcs_kernels.hip k_service) that
-// leaves after idle_us without a request or, between requests, after
-// 2 * idle_us of life.  The host tracks both clocks from its side
-// (conservatively: the kernel starts after its launch call and restarts its
-// idle clock before the host sees the verdicts); while it is sure, by a
-// margin of idle_us / 4, that the kernel is still waiting, a request is one
-// mailbox write and a wait on the verdicts.  Otherwise it starts the next
-// generation (queued behind the old kernel, which leaves at the new
-// generation's first request).  The mailbox is allocated at the first start
-// on a device and kept for the life of the process, so an asynchronous
-// request still in flight when the service stops can never read freed memory:
-// it finds the service off and re-runs its pages on the launch path.
+// device, with `lines` request lines (pcs_service_start_ex; 1 by default).  A
+// request (a synchronous validate / stamp call, or an asynchronous
+// pcs_batch) claims a free line with an atomic flag, writes the request
+// words, posts seq, and is answered through the line's verdict words; the
+// flag is released when the owner has read its results.  A call that finds
+// every line owned takes the launch path instead of queueing, so threads
+// never starve on a line.  Requests are served by a resident kernel
+// (pcs_kernels.hip k_service) with `wpl` workgroups per line; a workgroup
+// leaves after idle_us without a request on its line or, between requests,
+// after 2 * idle_us of life.  The host tracks those clocks from its side
+// (conservatively: the kernel starts after its launch call and restarts a
+// line's idle clock before the host sees the verdicts); while it is sure, by
+// a margin of idle_us / 4, that the line's workgroups still wait, a request
+// is one mailbox write and a wait on the verdicts.  Otherwise it starts the
+// next generation: the box names it first, so every workgroup of the old
+// kernel leaves at its next poll, and the new kernel, queued behind the old
+// one, starts once they have.
+//
+// A request is only ever served by the workgroups of its own generation, and
+// it is re-posted under a newer generation only once the kernel of the
+// generation it was posted to has left (an event recorded behind each
+// service kernel says so).  So no workgroup can still be writing a request's
+// verdicts after its owner has read them and released the line.
+//
+// The mailbox is allocated at a device's first start and kept for the life
+// of the process, so an asynchronous request still in flight when the
+// service stops can never read freed memory: it finds the service off and
+// re-runs its pages on the launch path.
+constexpr int kServiceEvents = 16;  // ring of events, one per generation (gen % 16)
 struct Service {
     using clock = std::chrono::steady_clock;
-    std::mutex mu;                 // everything below except line / callers / load; never held while waiting
-    std::atomic<int> line{0};      // 1 while a request owns the mailbox
+    struct Line {
+        std::atomic<int> owner{0};  // 1 while a request owns the line
+        uint32_t count = 0;         // requests posted on it (low half of seq)
+        clock::time_point answered;  // when its last request was answered (>= its workgroups' idle clock)
+    };
+    std::mutex mu;                 // everything below except the atomics; never held while waiting
     std::atomic<int> callers{0};   // eligible calls in progress on this device, on either path
     std::atomic<int> load{0};      // decaying average of `callers` seen at entry, x256
+    std::atomic<bool> gate_closed{false};  // the contention gate's state (with hysteresis)
     std::atomic<int> device{-1};   // -1: off (read without the lock by the entry points)
-    int workgroups = 0;
+    int lines = 0, wpl = 0;        // request lines, workgroups per line
     uint32_t idle_us = 0;
-    hipStream_t stream = nullptr;  // recreated at start unless a request still owns the line
+    hipStream_t stream = nullptr;  // recreated at start unless a request still owns a line
+    hipEvent_t done[kServiceEvents] = {};  // done[g % 16]: recorded behind generation g's kernel
     pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped; never freed
     pcs::ServiceBox* d = nullptr;  // its device alias
     uint32_t gen = 0;              // generation of the newest queued kernel (never reset)
-    uint32_t count = 0;            // requests posted to it
     bool live = false;             // it has been queued (it may have left since)
-    clock::time_point launched, answered;
+    clock::time_point launched;
+    Line line[pcs::kServiceMaxLines];
 };
 constexpr int kServiceDevices = 64;
 Service g_services[kServiceDevices];
@@ -550,7 +567,8 @@ std::atomic<int> g_services_on{0};  // devices with a service: the validate / st
 // the service's stream at the highest priority (HIP pools its hardware queues
 // by priority); under 4-16 threads of small batches that kept every thread
 // served (tools/lab/service_load.cpp, profiles/r03/service_load_*.txt).
-// 0: a plain stream.  A CU-masked stream is not offered.
+// 0: a plain stream.  A CU-masked stream is not offered: a resident kernel on
+// one blocks the creation of other threads' streams.
 hipError_t service_stream(hipStream_t* s) {
     if (pcs::get_tuning(PCS_TUNE_SERVICE_STREAM) == 1) {
         int lo = 0, hi = 0;
@@ -561,41 +579,47 @@ hipError_t service_stream(hipStream_t* s) {
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
+// Queue generation gen + 1: the box names it first, so the old kernel's
+// workgroups leave at their next poll; the new kernel is queued behind them.
 int service_launch_locked(Service& sv) {
     ++sv.gen;
-    sv.count = 0;
+    __atomic_store_n(&sv.h->gen, (uint64_t)sv.gen, __ATOMIC_RELEASE);
     sv.live = true;
-    sv.launched = sv.answered = Service::clock::now();
-    return finish(pcs::run_service(sv.d, sv.workgroups, sv.gen, (uint64_t)sv.idle_us * 100,
-                                   (uint64_t)sv.idle_us * 200, sv.stream),
-                  "service kernel launch");
+    sv.launched = Service::clock::now();
+    for (int k = 0; k < sv.lines; ++k) sv.line[k].answered = sv.launched;
+    hipError_t e = pcs::run_service(sv.d, sv.lines, sv.wpl, sv.gen, (uint64_t)sv.idle_us * 100,
+                                    (uint64_t)sv.idle_us * 200, sv.stream);
+    if (e == hipSuccess) e = hipEventRecord(sv.done[sv.gen % kServiceEvents], sv.stream);
+    return finish(e, "service kernel launch");
 }
 
-// Certainly still waiting: launched less than life - margin ago and last
-// answered less than idle - margin ago (host time bounds the kernel's clocks).
-bool service_waiting(const Service& sv, Service::clock::time_point now) {
+// Line k's workgroups certainly still wait: launched less than life - margin
+// ago and the line last answered less than idle - margin ago (host time
+// bounds the kernel's clocks).
+bool service_waiting(const Service& sv, int k, Service::clock::time_point now) {
     const auto margin = std::chrono::microseconds(sv.idle_us / 4);
     return sv.live && now - sv.launched < std::chrono::microseconds(2 * (uint64_t)sv.idle_us) - margin &&
-           now - sv.answered < std::chrono::microseconds(sv.idle_us) - margin;
+           now - sv.line[k].answered < std::chrono::microseconds(sv.idle_us) - margin;
 }
 
-// The check word of the request words as they now stand in the mailbox,
-// with `seq` in word 0 (service_word_mix, eloqstore_pcs_internal.h).
-uint64_t service_check(const pcs::ServiceBox* h, uint64_t seq) {
-    const uint64_t* w = &h->seq;
+// The check word of line `ln`'s request words as they now stand, with `seq`
+// in word 0 (service_word_mix, eloqstore_pcs_internal.h).
+uint64_t service_check(const pcs::ServiceLine* ln, uint64_t seq) {
+    const uint64_t* w = &ln->seq;
     uint64_t c = pcs::service_word_mix(seq, 0);
     for (int i = 1; i < pcs::kServiceLineWords; ++i)
         if (i != pcs::kServiceCheckWord) c += pcs::service_word_mix(w[i], (uint64_t)i);
     return c;
 }
 
-// Post the request words already in the mailbox under the next seq: the
+// Post the request words already on line k under the current generation: the
 // check word, then seq last.
-uint64_t service_post_locked(Service& sv) {
-    const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.count;
-    sv.h->check = service_check(sv.h, seq);
+uint64_t service_post_locked(Service& sv, int k) {
+    pcs::ServiceLine* ln = &sv.h->line[k];
+    const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.line[k].count;
+    ln->check = service_check(ln, seq);
     std::atomic_thread_fence(std::memory_order_release);
-    __atomic_store_n(&sv.h->seq, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&ln->seq, seq, __ATOMIC_RELEASE);
     return seq;
 }
 
@@ -611,7 +635,7 @@ hipError_t drain_bounded(hipStream_t s, std::chrono::milliseconds limit) {
 }
 
 // End every queued kernel (stop word, then a bounded drain) so none can still
-// read the request line when it is next rewritten; the next request starts a
+// read a request line when it is next rewritten; the next request starts a
 // new generation.
 hipError_t service_reset_locked(Service& sv) {
     __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);
@@ -661,15 +685,17 @@ constexpr int kTuneServiceTearTest = PCS_TUNE_SERVICE_TEAR_TEST;
 // PCS_TUNE_SERVICE_MAX_CALLERS: the contention gate (below).
 constexpr int kTuneServiceMaxCallers = PCS_TUNE_SERVICE_MAX_CALLERS;
 
-// Contention gate.  With several threads per GPU the one request line is
-// mostly owned by another thread, the calls that find it busy launch anyway,
-// and the resident kernel only widens the tail.  Every
-// eligible call counts itself in `callers` for its whole duration, on either
-// path, and folds the count it saw at entry into a decaying average (1/16 per
-// call); while the average exceeds PCS_TUNE_SERVICE_MAX_CALLERS + 0.5 the
-// service declines and the calls launch.  Counting calls on both paths keeps
-// the signal alive while the gate is closed, so it reopens only when the
-// callers thin out; the kernel idles out meanwhile and frees its CUs.
+// Contention gate.  With more threads than request lines on a GPU the lines
+// are mostly owned by other threads, the calls that find them busy launch
+// anyway, and the resident kernel only widens the tail.
+// Every eligible call counts itself in `callers` for its whole duration, on
+// either path, and folds the count it saw at entry into a decaying average
+// (1/16 per call); once the average exceeds PCS_TUNE_SERVICE_MAX_CALLERS +
+// lines - 1 + 0.5 the service declines and the calls launch, until it drops
+// below that limit - 0.5.  Counting calls
+// on both paths keeps the signal alive while the gate is closed, so it
+// reopens only when the callers thin out; the kernel idles out meanwhile and
+// frees its CUs.
 void caller_enter(Service& sv) {
     const int c = sv.callers.fetch_add(1, std::memory_order_relaxed) + 1;
     const int a = sv.load.load(std::memory_order_relaxed);
@@ -695,15 +721,27 @@ private:
     Service* sv_;
 };
 
-bool service_gate_open(const Service& sv) {
+// With hysteresis: the gate closes above limit + 0.5 and reopens only below
+// limit - 0.5, so a caller count near the limit does not flap between the
+// paths (a flapping gate relaunches the idled-out kernel again and again:
+// p99 54.7 µs at 4 threads on 2 lines, profiles/r04/service_load_wpl.txt).
+bool service_gate_open(Service& sv) {
     const int64_t m = pcs::get_tuning(kTuneServiceMaxCallers);
-    return m <= 0 || sv.load.load(std::memory_order_relaxed) <= (int)(m << 8) + 128;
+    if (m <= 0) return true;
+    const int limit = (int)((m + sv.lines - 1) << 8);
+    const int a = sv.load.load(std::memory_order_relaxed);
+    bool closed = sv.gate_closed.load(std::memory_order_relaxed);
+    if (!closed && a > limit + 128) sv.gate_closed.store(closed = true, std::memory_order_relaxed);
+    else if (closed && a < limit - 128) sv.gate_closed.store(closed = false, std::memory_order_relaxed);
+    return !closed;
 }
 
 // One request through the service, from claim to release.
 struct ServiceReq {
-    Service* sv = nullptr;  // set while the request owns the line
+    Service* sv = nullptr;  // set while the request owns a line
+    int k = 0;              // its line
     uint64_t n = 0, landed = 0, seq = 0;
+    uint32_t gen = 0;       // the generation it is posted to
     bool stamp = false;
     int relaunched = 0;
     Service::clock::time_point posted, checked;
@@ -711,42 +749,56 @@ struct ServiceReq {
 
 void service_release(ServiceReq& r) {
     if (!r.sv) return;
-    r.sv->line.store(0, std::memory_order_release);
+    r.sv->line[r.k].owner.store(0, std::memory_order_release);
     r.sv = nullptr;
 }
 
 std::atomic<uint64_t> g_torn_requests{0};
+thread_local int t_line_hint = -1;  // the line this thread used last: its first try
 
-// Claim the line and post a validate (stamp = false) or stamp request: XXH3,
-// registered 16-byte-aligned pages with page_size % 256 == 0, 1..256 pages, on
-// the calling thread's device with its service on and the gate open.
-// PCS_OK: posted, r owns the line.  kNotServed: nothing done.  < 0: error.
+// Claim a free line and post a validate (stamp = false) or stamp request:
+// XXH3, registered 16-byte-aligned pages with page_size % 256 == 0, 1..256
+// pages, on the calling thread's device with its service on and the gate
+// open.  PCS_OK: posted, r owns the line.  kNotServed: nothing done.  < 0:
+// error.
 int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64_t P, uint64_t n, int algo,
                    bool stamp) {
     if (!svp || algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
         return kNotServed;
     Service& sv = *svp;
     if (!service_gate_open(sv)) return kNotServed;
-    int expect = 0;
-    if (!sv.line.compare_exchange_strong(expect, 1, std::memory_order_acquire)) return kNotServed;
+    const int nl = std::max(1, std::min(sv.lines, pcs::kServiceMaxLines));  // racy read: revalidated below
+    int k = -1;
+    const int h0 = t_line_hint >= 0 ? t_line_hint : 0;
+    for (int i = 0; i < nl && k < 0; ++i) {
+        const int c = (h0 + i) % nl;
+        int expect = 0;
+        if (sv.line[c].owner.load(std::memory_order_relaxed) == 0 &&
+            sv.line[c].owner.compare_exchange_strong(expect, 1, std::memory_order_acquire))
+            k = c;
+    }
+    if (k < 0) return kNotServed;
     std::unique_lock<std::mutex> lk(sv.mu);
-    if (sv.device < 0) {
-        sv.line.store(0, std::memory_order_release);
+    if (sv.device < 0 || k >= sv.lines) {
+        sv.line[k].owner.store(0, std::memory_order_release);
         return kNotServed;
     }
+    pcs::ServiceLine* ln = &sv.h->line[k];
     const int64_t tear_us = pcs::get_tuning(kTuneServiceTearTest);
     uint64_t local[pcs::kServiceMaxPages];
-    uint64_t* dst = tear_us > 0 ? local : sv.h->ptrs;
+    uint64_t* dst = tear_us > 0 ? local : ln->ptrs;
     if (!g_regions.translate(pages, n, P, dst)) {
-        sv.line.store(0, std::memory_order_release);
+        sv.line[k].owner.store(0, std::memory_order_release);
         return kNotServed;
     }
+    t_line_hint = k;
     r = ServiceReq{};
     r.sv = &sv;
+    r.k = k;
     r.n = n;
     r.stamp = stamp;
-    for (uint64_t i = 0; i < n; ++i) sv.h->ok[i] = pcs::kServicePending;
-    if (!service_waiting(sv, Service::clock::now()))
+    for (uint64_t i = 0; i < n; ++i) ln->ok[i] = pcs::kServicePending;
+    if (!service_waiting(sv, k, Service::clock::now()))
         if (int rc = service_launch_locked(sv)) {
             (void)service_reset_locked(sv);
             service_release(r);
@@ -756,22 +808,23 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
     if (tear_us > 0) {
         // seq first, the request words after it, the check word last: until
         // then every poll sees the new seq beside the previous request's words
-        const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.count;
+        const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.line[k].count;
         std::atomic_thread_fence(std::memory_order_release);
-        __atomic_store_n(&sv.h->seq, seq, __ATOMIC_RELEASE);
+        __atomic_store_n(&ln->seq, seq, __ATOMIC_RELEASE);
         std::this_thread::sleep_for(std::chrono::microseconds(tear_us));
-        std::memcpy(sv.h->ptrs, local, n * 8);
-        sv.h->n = n;
-        sv.h->page_size = page_word;
-        const uint64_t c = service_check(sv.h, seq);
+        std::memcpy(ln->ptrs, local, n * 8);
+        ln->n = n;
+        ln->page_size = page_word;
+        const uint64_t c = service_check(ln, seq);
         std::atomic_thread_fence(std::memory_order_release);
-        __atomic_store_n(&sv.h->check, c, __ATOMIC_RELEASE);
+        __atomic_store_n(&ln->check, c, __ATOMIC_RELEASE);
         r.seq = seq;
     } else {
-        sv.h->n = n;
-        sv.h->page_size = page_word;
-        r.seq = service_post_locked(sv);
+        ln->n = n;
+        ln->page_size = page_word;
+        r.seq = service_post_locked(sv, k);
     }
+    r.gen = sv.gen;
     r.posted = r.checked = Service::clock::now();
     return PCS_OK;
 }
@@ -782,7 +835,7 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
 // the line), < 0 error.
 int service_progress(ServiceReq& r) {
     Service& sv = *r.sv;
-    const volatile uint32_t* v = sv.h->ok;
+    const volatile uint32_t* v = sv.h->line[r.k].ok;
     while (r.landed < r.n && v[r.landed] != pcs::kServicePending) ++r.landed;
     if (r.landed == r.n) {
         std::atomic_thread_fence(std::memory_order_acquire);
@@ -791,32 +844,38 @@ int service_progress(ServiceReq& r) {
     const auto now = Service::clock::now();
     if (now - r.checked < std::chrono::microseconds(50)) return 0;
     r.checked = now;
-    const hipError_t q = hipStreamQuery(sv.stream);  // the stream outlives every line owner
+    std::lock_guard<std::mutex> lk(sv.mu);
+    // Has the kernel of the generation this request was posted to left?  (Its
+    // event; a newer generation's event in the same ring slot is later on
+    // the stream, so its completion implies this one's.)
+    const hipError_t q = hipEventQuery(sv.done[r.gen % kServiceEvents]);
     if (q == hipErrorNotReady) {
         if (now - r.posted < std::chrono::seconds(5)) return 0;
-        std::lock_guard<std::mutex> lk(sv.mu);
         (void)service_reset_locked(sv);  // no answer in 5 s: a latency problem, not a failure
         return kFallback;
     }
-    std::lock_guard<std::mutex> lk(sv.mu);
     if (q != hipSuccess) {
         (void)service_reset_locked(sv);
         return hip_fail(q, "service stream");
     }
-    // every queued kernel has left with this request not fully answered (a
-    // workgroup reached its limit just before the post, or the service was
-    // stopped): verdicts are idempotent, so a new generation serves it again
+    // That kernel has left and this request is not fully answered (its
+    // workgroups reached a limit just before the post, a newer generation
+    // replaced it, or the service was stopped): no workgroup can write this
+    // line any more, and verdicts are idempotent, so the request is posted
+    // again to the current generation (started now if none is waiting).
     while (r.landed < r.n && v[r.landed] != pcs::kServicePending) ++r.landed;
     if (r.landed == r.n) {
         std::atomic_thread_fence(std::memory_order_acquire);
         return 1;
     }
-    if (sv.device < 0 || ++r.relaunched > 2) return kFallback;
-    if (int rc = service_launch_locked(sv)) {
-        (void)service_reset_locked(sv);
-        return rc;
-    }
-    r.seq = service_post_locked(sv);
+    if (sv.device < 0 || ++r.relaunched > 3) return kFallback;
+    if (r.gen == sv.gen || !service_waiting(sv, r.k, now))
+        if (int rc = service_launch_locked(sv)) {
+            (void)service_reset_locked(sv);
+            return rc;
+        }
+    r.seq = service_post_locked(sv, r.k);
+    r.gen = sv.gen;
     r.posted = Service::clock::now();
     return 0;
 }
@@ -824,22 +883,23 @@ int service_progress(ServiceReq& r) {
 // After progress returned 1: verdicts (validate) or the done words (stamp).
 int service_collect(ServiceReq& r, uint8_t* ok, uint64_t* first_bad) {
     Service& sv = *r.sv;
+    const pcs::ServiceLine* ln = &sv.h->line[r.k];
     {
         std::lock_guard<std::mutex> lk(sv.mu);
-        sv.answered = Service::clock::now();
+        sv.line[r.k].answered = Service::clock::now();
     }
-    if (__atomic_load_n(&sv.h->torn_seq, __ATOMIC_RELAXED) == r.seq)
+    if (__atomic_load_n(&ln->torn_seq, __ATOMIC_RELAXED) == r.seq)
         g_torn_requests.fetch_add(1, std::memory_order_relaxed);
     if (!r.stamp) {
         uint64_t bad = UINT64_MAX;
         for (uint64_t i = 0; i < r.n; ++i) {
-            ok[i] = (uint8_t)sv.h->ok[i];
+            ok[i] = (uint8_t)ln->ok[i];
             if (!ok[i] && bad == UINT64_MAX) bad = i;
         }
         if (first_bad) *first_bad = bad;
     } else {
         for (uint64_t i = 0; i < r.n; ++i)
-            if (sv.h->ok[i] != 1u) return fail(PCS_ERR_HIP, "validate service: stamp not confirmed");
+            if (ln->ok[i] != 1u) return fail(PCS_ERR_HIP, "validate service: stamp not confirmed");
     }
     count(PCS_COUNTER_SERVICE_BATCHES);
     return PCS_OK;
@@ -1155,8 +1215,13 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
 }
 
-int pcs_service_start(int workgroups, uint32_t idle_us) {
-    if (workgroups < 1 || workgroups > 256) return fail(PCS_ERR_INVALID, "workgroups must be in [1, 256]");
+int pcs_service_start(int workgroups, uint32_t idle_us) { return pcs_service_start_ex(1, workgroups, idle_us); }
+
+int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us) {
+    if (lines < 1 || lines > pcs::kServiceMaxLines)
+        return fail(PCS_ERR_INVALID, "lines must be in [1, " + std::to_string(pcs::kServiceMaxLines) + "]");
+    if (workgroups_per_line < 1 || lines * workgroups_per_line > 256)
+        return fail(PCS_ERR_INVALID, "workgroups must be in [1, 256] (lines x workgroups per line)");
     if (idle_us && (idle_us < 200 || idle_us > 1000000))
         return fail(PCS_ERR_INVALID, "idle_us must be 0 (1000) or in [200, 1000000]");
     if (int rc = require_device()) return rc;
@@ -1169,9 +1234,11 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "service start");
     // The stream is recreated (PCS_TUNE_SERVICE_STREAM is read here) unless
-    // an asynchronous request of the previous run still owns the line and
-    // may query it; the mailbox is allocated once and kept.
-    if (sv.stream && sv.line.load(std::memory_order_acquire) == 0) {
+    // an asynchronous request of the previous run still owns a line and may
+    // be waiting on its kernel; the mailbox and the events are made once.
+    bool owned = false;
+    for (auto& l : sv.line) owned |= l.owner.load(std::memory_order_acquire) != 0;
+    if (sv.stream && !owned) {
         (void)hipStreamDestroy(sv.stream);
         sv.stream = nullptr;
     }
@@ -1179,6 +1246,11 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
         sv.stream = nullptr;
         return hip_fail(e, "service start");
     }
+    for (auto& ev : sv.done)
+        if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
+            ev = nullptr;
+            return hip_fail(e, "service start (events)");
+        }
     if (!sv.h) {
         pcs::ServiceBox* h = nullptr;
         if (hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(pcs::ServiceBox),
@@ -1193,10 +1265,14 @@ int pcs_service_start(int workgroups, uint32_t idle_us) {
         sv.h = h;
         sv.d = d;
     }
-    sv.workgroups = workgroups;
+    // a line still owned by a request of the previous run stays out of use
+    // until that request is released (its owner re-runs it on the launch path)
+    sv.lines = lines;
+    sv.wpl = workgroups_per_line;
     sv.idle_us = idle_us ? idle_us : 1000;
     sv.live = false;
     sv.load.store(0, std::memory_order_relaxed);
+    sv.gate_closed.store(false, std::memory_order_relaxed);
     sv.device = dev;
     g_services_on.fetch_add(1, std::memory_order_relaxed);
     static std::once_flag hook;

@@ -1862,66 +1862,69 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // host starts the next generation of it when it can no longer be sure one is
 // waiting.  A kernel serves only requests of its own generation (the high 32
 // bits of seq), so a late kernel of an earlier generation never serves a
-// request twice, and leaves at the first request of a newer one, so the next
-// kernel (queued behind it on the stream) starts at once.  16 lanes of each
-// workgroup poll the request words (eloqstore_pcs_internal.h: seq, n,
-// page_size, check, ptrs[0..12)) with one 8-byte load each.  Those loads are
-// separate, so a poll can see the new seq beside an older request's words:
-// the workgroup serves a request only when the 15 words' mixes add up to the
-// check word the host wrote with them, and otherwise reads the line again
-// (a torn view of one request is ignored, never served).  Then it runs a
-// system-scope acquire (pages and ptrs[12..n) are read fresh from host memory,
-// ordered after the seq that announced them), hashes pages blockIdx.x * 16 +
-// group, stride gridDim.x * 16 (the run-time-size XXH3 body: registered
-// 16-byte-aligned pages, page_size % 256 == 0) and stores each verdict word
-// system-scope, which reaches host memory without a release fence.  A stamp
-// request (high half of the page-size word) stores the digest into the page
-// header instead and then a done word, released after it.
-__global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, uint64_t idle_ticks,
+// request twice, and leaves as soon as the box names a newer one, so the next
+// kernel (queued behind it on the stream) starts at once.  Workgroup w
+// serves request line w / wpl, as the (w % wpl)-th of the line's wpl
+// workgroups.  18 of its lanes poll: 16 load the line's request words (seq,
+// n, page_size, check, ptrs[0..12), eloqstore_pcs_internal.h) and two the
+// box's stop and gen words, one 8-byte load each.  Those loads are separate,
+// so a poll can see the new seq beside an older request's words: the
+// workgroup serves a request only when the 15 words' mixes add up to the
+// check word the host wrote with them, and otherwise reads the line again (a
+// torn view of one request is ignored, never served).  A request of another
+// generation is not this kernel's (the host re-posts it once its own kernel
+// has left).  Then the polling lanes run a system-scope acquire (pages and
+// ptrs[12..n) are read fresh from host memory, ordered after the seq that
+// announced them), and the workgroup hashes pages j * 16 + group, stride
+// wpl * 16 (the run-time-size XXH3 body: registered 16-byte-aligned pages,
+// page_size % 256 == 0), storing each verdict word system-scope, which
+// reaches host memory without a release fence.  A stamp request (high half
+// of the page-size word) stores the digest into the page header instead and
+// then a done word, released after it.
+__global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint64_t gen, uint64_t idle_ticks,
                                                  uint64_t life_ticks) {
     constexpr int W = kServiceLineWords;
     __shared__ uint64_t s_line[W];
     __shared__ int s_go;
+    ServiceLine* line = &box->line[blockIdx.x / wpl];
+    const int j = blockIdx.x % wpl;
     const Xxh3Lane L = make_xxh3_lane(threadIdx.x & 15);
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
     uint64_t t_last = born;
-    uint64_t last = gen << 32;  // this generation's requests carry gen << 32 | count, count from 1
+    uint64_t last = 0;  // the last seq this workgroup served
     uint64_t torn_noted = 0;
     for (;;) {
-        if (threadIdx.x < W) {
-            const uint64_t* line = &box->seq;
+        if (threadIdx.x < W + 2) {
+            const uint64_t* src = threadIdx.x < W ? &line->seq + threadIdx.x : &box->stop + (threadIdx.x - W);
             uint64_t w = 0;
             int go = 0;
             for (;;) {
-                w = __hip_atomic_load(line + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const uint64_t w0 = __shfl(w, 0, W);
-                if (w0 != last) {
-                    // a request of a newer generation: the host has moved on
-                    // (every request of this one is answered) and the next
-                    // kernel, queued behind this one, starts once it leaves
-                    if ((w0 >> 32) != gen) break;
-                    uint64_t m = threadIdx.x == kServiceCheckWord ? 0 : service_word_mix(w, threadIdx.x);
+                w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t w0 = __shfl(w, 0, 32);
+                // stop, or a newer generation queued behind this kernel
+                if (__shfl(w, W, 32) != 0 || __shfl(w, W + 1, 32) != gen) break;
+                if (w0 != last && (w0 >> 32) == gen) {
+                    uint64_t m = threadIdx.x == kServiceCheckWord || threadIdx.x >= W ? 0 : service_word_mix(w, threadIdx.x);
 #pragma unroll
                     for (int d = 1; d < W; d <<= 1) m += __shfl_xor(m, d, W);
-                    if (m == __shfl(w, kServiceCheckWord, W)) {
+                    // lane 0's sum for all 18 lanes, so every decision below is uniform
+                    if (__shfl(m, 0, 32) == __shfl(w, kServiceCheckWord, 32)) {
                         go = 1;
                         break;
                     }
                     // torn: seq is new, some word is not yet this request's
-                    if (blockIdx.x == 0 && threadIdx.x == 0 && torn_noted != w0) {
+                    if (j == 0 && threadIdx.x == 0 && torn_noted != w0) {
                         torn_noted = w0;
-                        __hip_atomic_store(&box->torn_seq, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(&line->torn_seq, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (__hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                    now - t_last > idle_ticks || now - born > life_ticks)
-                    break;
+                if (now - t_last > idle_ticks || now - born > life_ticks) break;
             }
             // acquire here, in the lanes whose loads saw the new seq; the
             // barrier then orders every lane's reads after it
             if (go) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            s_line[threadIdx.x] = w;
+            if (threadIdx.x < W) s_line[threadIdx.x] = w;
             if (threadIdx.x == 0) s_go = go;
         }
         __syncthreads();
@@ -1931,10 +1934,10 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, 
         const uint32_t P = (uint32_t)s_line[2];
         const bool stamp = (s_line[2] >> 32) != 0;  // kServiceStamp: write the digest into the header
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        for (uint64_t pg = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 4); pg < n; pg += (uint64_t)gridDim.x * 16) {
+        for (uint64_t pg = (uint64_t)j * 16 + (threadIdx.x >> 4); pg < n; pg += (uint64_t)wpl * 16) {
             const uint64_t a = pg < (uint64_t)kServiceLinePtrs
                                    ? s_line[4 + pg]  // came with the checked poll
-                                   : __hip_atomic_load(&box->ptrs[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                   : __hip_atomic_load(&line->ptrs[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             uint64_t stored = 0;
             const uint64_t h = xxh3_page_rt4<false>(reinterpret_cast<const uint8_t*>(a), P, L, stored);
             if (L.g == 0) {
@@ -1942,9 +1945,9 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, 
                     // the header, then the done word released after it: the
                     // host sees the word only once the header has landed
                     __hip_atomic_store(reinterpret_cast<uint64_t*>(a), h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store(&box->ok[pg], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&line->ok[pg], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 } else {
-                    __hip_atomic_store(&box->ok[pg], h == stored ? 1u : 0u, __ATOMIC_RELAXED,
+                    __hip_atomic_store(&line->ok[pg], h == stored ? 1u : 0u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
@@ -1954,11 +1957,11 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, uint64_t gen, 
     }
 }
 
-hipError_t run_service(ServiceBox* d_box, int workgroups, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                        hipStream_t s) {
-    if (workgroups < 1 || workgroups > 256) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_service, dim3((unsigned)workgroups), dim3(kBlock), 0, s, d_box, (uint64_t)gen, idle_ticks,
-                       life_ticks);
+    if (lines < 1 || lines > kServiceMaxLines || wpl < 1 || lines * wpl > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_service, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, (uint64_t)gen,
+                       idle_ticks, life_ticks);
     return hipGetLastError();
 }
 

@@ -118,12 +118,14 @@ void UnregisterPagePool(void* base);
 // loop from 20-24 pages to validate and 28-32 to stamp).  The kernel holds
 // `workgroups` CUs (16 serves 128-256 pages 10-15 % faster than 4) and
 // leaves after idle_us without a request or 2 * idle_us of life; the next
-// request starts a new one.  One request line per device: a call that finds
-// it owned, or that arrives while more than PCS_TUNE_SERVICE_MAX_CALLERS
-// eligible calls are in progress on the device (a decaying average; 2 by
-// default), takes the launch path.  Start and stop act on the calling
-// thread's current device; each device has its own service.
-void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000);
+// request starts a new one.  `lines` request lines (1-8) let that many calls
+// be served at once, each line by its own `workgroups` workgroups.  A call
+// that finds every line owned, or that arrives while more than
+// PCS_TUNE_SERVICE_MAX_CALLERS + lines - 1 eligible calls are in progress on
+// the device (a decaying average; the knob is 2 by default), takes the launch
+// path.  Start and stop act on the calling thread's current device; each
+// device has its own service.
+void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000, int lines = 1);
 void StopChecksumService();
 inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(128) << 10;
 

@@ -214,8 +214,12 @@ int pcs_batch_destroy(pcs_batch *b);
  * regions, 16-byte aligned, page_size % 256 == 0, called on a device whose
  * service is on; everything else takes the launch path.  Each device has its
  * own service: pcs_service_start / stop / running act on the calling
- * thread's current device (pcs_set_device).  One request per device is in
- * flight at a time (calls from several threads serialise).  The kernel leaves
+ * thread's current device (pcs_set_device).  One request per request line is
+ * in flight at a time (one line by default, up to 8 with
+ * pcs_service_start_ex); a call that finds every line owned, or arrives while
+ * more eligible calls are in progress on the device than
+ * PCS_TUNE_SERVICE_MAX_CALLERS + lines - 1 (a decaying average), takes the
+ * launch path.  The kernel leaves
  * after idle_us (0 = 1000; else 200 .. 1000000) without a request and, between
  * requests, after 2 * idle_us of life, and the next request starts a new one:
  * it holds its CUs, and delays any device-synchronising HIP call of the
@@ -224,6 +228,11 @@ int pcs_batch_destroy(pcs_batch *b);
  * an idle_us out of range, or when the device's service is already running.
  * Services still running at exit are stopped by an atexit handler. */
 int pcs_service_start(int workgroups, uint32_t idle_us);
+/* The same with `lines` request lines (1 .. 8), each served by its own
+ * `workgroups_per_line` workgroups (lines x workgroups_per_line <= 256): up
+ * to `lines` calls on the device are in flight through the service at once,
+ * each on a line of its own.  pcs_service_start(wg, idle) = _ex(1, wg, idle). */
+int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us);
 int pcs_service_stop(void);
 int pcs_service_running(void); /* 1 while the service is on, 0 otherwise */
 
@@ -292,8 +301,9 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_SERVICE_MAX_CALLERS  [2] validate service contention gate: while
  *                                     the decaying average of concurrent
  *                                     eligible calls on the device exceeds
- *                                     this + 0.5, the service declines and
- *                                     calls take the launch path; 0 = off
+ *                                     this + lines - 1 + 0.5, the service
+ *                                     declines and calls take the launch
+ *                                     path; 0 = off
  *   PCS_TUNE_SERVICE_TEAR_TEST    [0] test only: microseconds the service's
  *                                     host side waits between posting seq and
  *                                     writing the request words (the kernel

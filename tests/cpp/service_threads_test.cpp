@@ -14,7 +14,9 @@
 //      request named keep a zero header;
 //   4. the contention gate at its default (2): one thread is always served;
 //      eight threads drive the caller average over the limit and the service
-//      declines nearly everything (launch path), verdicts exact.
+//      declines nearly everything (launch path), verdicts exact;
+//   5. four request lines (pcs_service_start_ex): eight threads exact with
+//      the gate off, four threads served on most calls with it on.
 // The CPU oracle is the checker.  Prints "service threads ok" on success.
 #include <atomic>
 #include <chrono>
@@ -188,6 +190,37 @@ int main() {
         std::printf("gate 2, %d threads: %llu requests, served share %.3f\n", threads,
                     (unsigned long long)calls.load(), share);
         CHECK(threads == 1 ? share == 1.0 : share < 0.2);
+    }
+
+    // 5: four request lines, two workgroups each: eight threads with the
+    // gate off stay exact on every path, and with the gate at its default
+    // four threads are served on most calls (one line each)
+    eloqstore::StopChecksumService();
+    eloqstore::StartChecksumService(2, 1000, 4);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 0) == PCS_OK);
+    for (int async = 0; async < 2; ++async) {
+        std::atomic<uint64_t> calls{0};
+        const Counts c0 = counts();
+        CHECK(run_validate(pool, T, 0.5, async, 48, calls) == 0);
+        const Counts c1 = counts();
+        const uint64_t served = c1.served - c0.served, launched = c1.launched - c0.launched;
+        CHECK(served + launched == calls.load() && served > 0);
+        std::printf("4 lines: %s validate, %d threads, gate off: %llu requests exact (%llu served, %llu launched)\n",
+                    async ? "async" : "sync", T, (unsigned long long)calls.load(), (unsigned long long)served,
+                    (unsigned long long)launched);
+    }
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
+    for (int threads : {4, 8}) {
+        std::atomic<uint64_t> calls{0};
+        run_validate(pool, threads, 0.1, false, 6, calls);
+        calls = 0;
+        const Counts c0 = counts();
+        CHECK(run_validate(pool, threads, 0.4, false, 6, calls) == 0);
+        const Counts c1 = counts();
+        const double share = (double)(c1.served - c0.served) / (double)calls.load();
+        std::printf("4 lines, gate 2, %d threads: %llu requests, served share %.3f\n", threads,
+                    (unsigned long long)calls.load(), share);
+        CHECK(threads == 4 ? share > 0.5 : share < 0.2);
     }
 
     eloqstore::StopChecksumService();

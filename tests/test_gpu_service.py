@@ -206,6 +206,78 @@ def test_service_alternating_page_sets(service):
         assert pcs.counter(SVC) == s0 + calls
 
 
+@pytest.mark.parametrize("lines,wpl", [(4, 2), (8, 1)])
+def test_service_lines_under_threads(lines, wpl, no_gate):
+    """pcs_service_start_ex: several request lines, each served by its own
+    workgroups.  Four threads, each request with a corrupted page of its own
+    (low slots mostly): exact verdicts and first_bad on whichever line or
+    path served it; the served share shows the lines were used."""
+    P, T, per = 4096, 4, 256
+    with stamped_pool(T * per, P, 0x5F6 + lines) as pool, pcs.ValidateService(wpl, 1000, lines):
+        errors = []
+
+        def worker(t):
+            rng = np.random.default_rng(500 + t)
+            try:
+                for _ in range(80):
+                    n = int(rng.integers(1, 40))
+                    idx = t * per + rng.permutation(per)[:n]
+                    k = int(rng.integers(0, min(n, 12)))
+                    pool.pages[idx[k], 8 + int(rng.integers(0, P - 8))] ^= 0x04
+                    ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                    want = np.ones(n, dtype=bool)
+                    want[k] = False
+                    if fb != k or not np.array_equal(ok.astype(bool), want):
+                        errors.append((t, n, k, fb))
+                    pcs.stamp_ptrs(pool.ptr(idx[k:k + 1]), P)
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        s0, z0 = counters()
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:5]
+        s1, z1 = counters()
+        assert s1 - s0 + z1 - z0 == 2 * T * 80
+        assert s1 - s0 > (z1 - z0), (s1 - s0, z1 - z0)  # with a line per thread, the service takes most calls
+
+
+def test_service_lines_torn_drill_and_async(no_gate):
+    """Four lines: the torn-line drill on every line in turn (two threads'
+    worth of async batches in flight at once, each on its own line) and
+    exact verdicts throughout."""
+    P = 4096
+    with stamped_pool(512, P, 0x5F7) as pool, pcs.ValidateService(1, 1000, 4):
+        torn0 = pcs.counter(pcs.COUNTER_SERVICE_TORN_REQUESTS)
+        pcs.set_tuning(pcs.TUNE_SERVICE_TEAR_TEST, 30)
+        b1, b2 = pcs.Batch(), pcs.Batch()
+        try:
+            for i in range(24):
+                i1, i2 = np.arange(i, i + 6), 256 + np.arange(3 * i, 3 * i + 20)
+                k1, k2 = i % 6, (5 * i) % 20
+                pool.pages[i1[k1], 100] ^= 0x01
+                pool.pages[i2[k2], 200] ^= 0x01
+                s0, _ = counters()
+                b1.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(i1), P)
+                b2.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(i2), P)
+                b2.wait()
+                b1.wait()
+                assert pcs.counter(SVC) == s0 + 2, i  # both served, each on a line of its own
+                ok1, fb1 = b1.result()
+                ok2, fb2 = b2.result()
+                pool.pages[i1[k1], 100] ^= 0x01
+                pool.pages[i2[k2], 200] ^= 0x01
+                assert fb1 == k1 and ok1.count(0) == 1 and fb2 == k2 and ok2.count(0) == 1, (i, fb1, fb2)
+        finally:
+            pcs.set_tuning(pcs.TUNE_SERVICE_TEAR_TEST, 0)
+            b1.close()
+            b2.close()
+        assert pcs.counter(pcs.COUNTER_SERVICE_TORN_REQUESTS) - torn0 >= 24
+
+
 def test_service_torn_line_drill(service):
     """PCS_TUNE_SERVICE_TEAR_TEST posts seq first and writes the request
     words 30 us later, so the waiting kernel's polls see the new seq beside
@@ -396,6 +468,9 @@ def test_service_lifecycle():
     for bad in ((0, 0), (257, 0), (4, 100), (4, 2000000)):
         with pytest.raises(pcs.PcsError):
             pcs._call("pcs_service_start", *bad)
+    for bad in ((0, 1, 0), (9, 1, 0), (4, 65, 0), (2, 0, 0), (2, 2, 100)):
+        with pytest.raises(pcs.PcsError):
+            pcs._call("pcs_service_start_ex", *bad)
     with stamped_pool(64, P, 0x5EC) as pool:
         ptrs = pool.ptr(np.arange(8))
         for _round in range(2):  # start, serve, stop, and again

@@ -210,11 +210,15 @@ int main(int argc, char** argv) {
     uint64_t total_bad = 0;
     // argv[2]: service runs, one letter-digit pair each: s<k> = gate off,
     // g<k> = gate at its default (2 callers), k = PCS_TUNE_SERVICE_STREAM
-    // (1 highest priority, 0 plain); default "s1g1".  argv[3]: batch sizes,
-    // comma-separated (default 6,32,128).
+    // (1 highest priority, 0 plain); L<n> / M<n> / N<n> = n request lines of
+    // one / two / four workgroups each, gate at its default, highest-priority
+    // stream; default "s1g1".
+    // argv[3]: batch sizes, comma-separated (default 6,32,128).
     const char* kinds = argc > 2 ? argv[2] : "s1g1";
     std::vector<int> modes = {kCpu, kLaunch};
-    for (const char* k = kinds; k[0] && k[1]; k += 2) modes.push_back((k[0] == 'g' ? 200 : 100) + (k[1] - '0'));
+    for (const char* k = kinds; k[0] && k[1]; k += 2)
+        modes.push_back((k[0] == 'g' ? 200 : k[0] == 'L' ? 300 : k[0] == 'M' ? 400 : k[0] == 'N' ? 500 : 100) +
+                        (k[1] - '0'));
     std::vector<size_t> sizes;
     for (const char* b = argc > 3 ? argv[3] : "6,32,128"; *b;) {
         sizes.push_back(std::strtoul(b, const_cast<char**>(&b), 10));
@@ -225,11 +229,13 @@ int main(int argc, char** argv) {
             for (int T : {1, 2, 4, 8, 16}) {
                 const Mode m = mm >= 100 ? kService : (Mode)mm;
                 const bool gated = mm >= 200;
+                const int lines = mm >= 300 ? mm % 100 : 1;
+                const int wpl = mm >= 500 ? 4 : mm >= 400 ? 2 : mm >= 300 ? 1 : 4;
                 if (m == kService) {
-                    pcs_set_tuning(PCS_TUNE_SERVICE_STREAM, mm % 100);
+                    pcs_set_tuning(PCS_TUNE_SERVICE_STREAM, mm >= 300 ? 1 : mm % 100);
                     pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, gated ? 2 : 0);
                     mark(0, kStartService);
-                    eloqstore::StartChecksumService(4, 1000);
+                    eloqstore::StartChecksumService(wpl, 1000, lines);
                     mark(0, kIdle);
                 }
                 const uint64_t served0 = pcs_counter(PCS_COUNTER_SERVICE_BATCHES);
@@ -248,7 +254,9 @@ int main(int argc, char** argv) {
                 total_bad += r.bad;
                 char name[16];
                 std::snprintf(name, sizeof name, "%s", m == kCpu ? "cpu" : "launch");
-                if (m == kService) std::snprintf(name, sizeof name, "%s%d", gated ? "gated" : "service", mm % 100);
+                if (m == kService)
+                    std::snprintf(name, sizeof name, "%s%d", mm >= 300 ? (wpl == 1 ? "L1x" : wpl == 2 ? "L2x" : "L4x")
+                                                                    : gated ? "gated" : "service", mm % 100);
                 std::printf("%-8s %5zu  %7d  %9.0f  %10.0f  %6.1f  %6.1f  %llu  %12.2f  %10llu  %10llu\n",
                             name, B, T, r.batches_per_s,
                             r.batches_per_s * B, r.p50_us, r.p99_us, (unsigned long long)r.bad,
