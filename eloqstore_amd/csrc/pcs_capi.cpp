@@ -545,13 +545,14 @@ struct Service {
     std::atomic<int> load{0};      // decaying average of `callers` seen at entry, x256
     std::atomic<bool> gate_closed{false};  // the contention gate's state (with hysteresis)
     std::atomic<int> device{-1};   // -1: off (read without the lock by the entry points)
-    int lines = 0, wpl = 0;        // request lines, workgroups per line
+    std::atomic<int> lines{0};     // request lines (read without the lock when claiming one)
+    int wpl = 0;                   // workgroups per line
     uint32_t idle_us = 0;
     hipStream_t stream = nullptr;  // recreated at start unless a request still owns a line
     hipEvent_t done[kServiceEvents] = {};  // done[g % 16]: recorded behind generation g's kernel
     pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped; never freed
     pcs::ServiceBox* d = nullptr;  // its device alias
-    uint32_t gen = 0;              // generation of the newest queued kernel (never reset)
+    std::atomic<uint32_t> gen{0};  // generation of the newest queued kernel (never reset; read unlocked)
     bool live = false;             // it has been queued (it may have left since)
     clock::time_point launched;
     Line line[pcs::kServiceMaxLines];
@@ -582,14 +583,15 @@ hipError_t service_stream(hipStream_t* s) {
 // Queue generation gen + 1: the box names it first, so the old kernel's
 // workgroups leave at their next poll; the new kernel is queued behind them.
 int service_launch_locked(Service& sv) {
-    ++sv.gen;
-    __atomic_store_n(&sv.h->gen, (uint64_t)sv.gen, __ATOMIC_RELEASE);
+    const uint32_t g = sv.gen.load(std::memory_order_relaxed) + 1;
+    __atomic_store_n(&sv.h->gen, (uint64_t)g, __ATOMIC_RELEASE);
+    sv.gen.store(g, std::memory_order_release);
     sv.live = true;
     sv.launched = Service::clock::now();
     for (int k = 0; k < sv.lines; ++k) sv.line[k].answered = sv.launched;
-    hipError_t e = pcs::run_service(sv.d, sv.lines, sv.wpl, sv.gen, (uint64_t)sv.idle_us * 100,
+    hipError_t e = pcs::run_service(sv.d, sv.lines, sv.wpl, g, (uint64_t)sv.idle_us * 100,
                                     (uint64_t)sv.idle_us * 200, sv.stream);
-    if (e == hipSuccess) e = hipEventRecord(sv.done[sv.gen % kServiceEvents], sv.stream);
+    if (e == hipSuccess) e = hipEventRecord(sv.done[g % kServiceEvents], sv.stream);
     return finish(e, "service kernel launch");
 }
 
@@ -616,7 +618,7 @@ uint64_t service_check(const pcs::ServiceLine* ln, uint64_t seq) {
 // check word, then seq last.
 uint64_t service_post_locked(Service& sv, int k) {
     pcs::ServiceLine* ln = &sv.h->line[k];
-    const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.line[k].count;
+    const uint64_t seq = (uint64_t)sv.gen.load(std::memory_order_relaxed) << 32 | ++sv.line[k].count;
     ln->check = service_check(ln, seq);
     std::atomic_thread_fence(std::memory_order_release);
     __atomic_store_n(&ln->seq, seq, __ATOMIC_RELEASE);
@@ -767,7 +769,7 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
         return kNotServed;
     Service& sv = *svp;
     if (!service_gate_open(sv)) return kNotServed;
-    const int nl = std::max(1, std::min(sv.lines, pcs::kServiceMaxLines));  // racy read: revalidated below
+    const int nl = std::max(1, std::min(sv.lines.load(std::memory_order_relaxed), pcs::kServiceMaxLines));
     int k = -1;
     const int h0 = t_line_hint >= 0 ? t_line_hint : 0;
     for (int i = 0; i < nl && k < 0; ++i) {
@@ -808,7 +810,7 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
     if (tear_us > 0) {
         // seq first, the request words after it, the check word last: until
         // then every poll sees the new seq beside the previous request's words
-        const uint64_t seq = (uint64_t)sv.gen << 32 | ++sv.line[k].count;
+        const uint64_t seq = (uint64_t)sv.gen.load(std::memory_order_relaxed) << 32 | ++sv.line[k].count;
         std::atomic_thread_fence(std::memory_order_release);
         __atomic_store_n(&ln->seq, seq, __ATOMIC_RELEASE);
         std::this_thread::sleep_for(std::chrono::microseconds(tear_us));
@@ -824,7 +826,7 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
         ln->page_size = page_word;
         r.seq = service_post_locked(sv, k);
     }
-    r.gen = sv.gen;
+    r.gen = sv.gen.load(std::memory_order_relaxed);
     r.posted = r.checked = Service::clock::now();
     return PCS_OK;
 }
@@ -841,8 +843,11 @@ int service_progress(ServiceReq& r) {
         std::atomic_thread_fence(std::memory_order_acquire);
         return 1;
     }
+    // The kernel's state is checked every 50 µs, and at once when a newer
+    // generation has been started (this request must then be re-posted as
+    // soon as its own generation's kernel has left).
     const auto now = Service::clock::now();
-    if (now - r.checked < std::chrono::microseconds(50)) return 0;
+    if (now - r.checked < std::chrono::microseconds(50) && r.gen == sv.gen.load(std::memory_order_acquire)) return 0;
     r.checked = now;
     std::lock_guard<std::mutex> lk(sv.mu);
     // Has the kernel of the generation this request was posted to left?  (Its
@@ -869,13 +874,13 @@ int service_progress(ServiceReq& r) {
         return 1;
     }
     if (sv.device < 0 || ++r.relaunched > 3) return kFallback;
-    if (r.gen == sv.gen || !service_waiting(sv, r.k, now))
+    if (r.gen == sv.gen.load(std::memory_order_relaxed) || !service_waiting(sv, r.k, now))
         if (int rc = service_launch_locked(sv)) {
             (void)service_reset_locked(sv);
             return rc;
         }
     r.seq = service_post_locked(sv, r.k);
-    r.gen = sv.gen;
+    r.gen = sv.gen.load(std::memory_order_relaxed);
     r.posted = Service::clock::now();
     return 0;
 }

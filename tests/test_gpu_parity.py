@@ -832,7 +832,9 @@ def test_xxh64_desc_sparse_offshape_pages():
         offs[i] = pos
         pos += int(lens[i])
         pos = (pos + 15) // 16 * 16
-    host = np.random.default_rng(64).integers(0, 256, size=pos + 64, dtype=np.uint8)
+    # room for both layouts: the packed one (shorter, one page is 1000 bytes)
+    # and the n x 4 KiB one below
+    host = np.random.default_rng(64).integers(0, 256, size=max(pos, n * P) + 64, dtype=np.uint8)
     base = torch.from_numpy(host).to(DEV)
     d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
     d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
