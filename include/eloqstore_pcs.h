@@ -304,6 +304,11 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     this + lines - 1 + 0.5, the service
  *                                     declines and calls take the launch
  *                                     path; 0 = off
+ *   PCS_TUNE_XXH64_RUNS           [0] XXH64 descriptor batches: 1 = each wave
+ *                                     cuts a window of 64 pages into 16
+ *                                     equal-byte runs, one quad hashing each
+ *                                     run (pages of a multiple of 256 bytes);
+ *                                     0 = one page per quad (k_xxh64_lds)
  *   PCS_TUNE_SERVICE_TEAR_TEST    [0] test only: microseconds the service's
  *                                     host side waits between posting seq and
  *                                     writing the request words (the kernel
@@ -337,6 +342,7 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_TEAR_TEST = 26,
     PCS_TUNE_FAIL_INJECT = 27,
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
+    PCS_TUNE_XXH64_RUNS = 29,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

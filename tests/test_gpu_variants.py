@@ -29,12 +29,14 @@ VARIANTS = {
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "x64_one_wave": {pcs.TUNE_XXH64_WAVES: 1},
     "x64_two_waves_depth4": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 4},
+    "x64_runs": {pcs.TUNE_XXH64_RUNS: 1},
+    "x64_runs_no_nt": {pcs.TUNE_XXH64_RUNS: 1, pcs.TUNE_NT_LOADS: 0},
 }
 
 
 @pytest.fixture
 def tuned(request):
-    keys = [k for k in range(1, 25) if pcs.get_tuning(k) >= 0]  # retired keys read -1
+    keys = [k for k in range(1, 30) if pcs.get_tuning(k) >= 0 and k not in (26, 27)]  # retired keys read -1
     saved = {k: pcs.get_tuning(k) for k in keys}
     for k, v in VARIANTS[request.param].items():
         pcs.set_tuning(k, v)
@@ -66,7 +68,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_one_wave",
-                                   "x64_two_waves_depth4"],
+                                   "x64_two_waves_depth4", "x64_runs", "x64_runs_no_nt"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):
@@ -95,10 +97,11 @@ def test_variant_mixed_desc(tuned, algo):
     assert int(fb.cpu().numpy().view(np.uint64)[0]) == 3
 
 
-@pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block"], indirect=True)
+@pytest.mark.parametrize("tuned,algo", [("default", 0), ("no_nt", 0), ("rt_one_block", 0), ("default", 1),
+                                        ("x64_runs", 1), ("x64_runs_no_nt", 1)], indirect=["tuned"])
 @pytest.mark.parametrize("mode", ["digest", "validate", "stamp"])
-def test_desc_mixed_with_leftovers(tuned, mode):
-    """XXH3 descriptor batches of every shape class: 4-16 KiB pages and
+def test_desc_mixed_with_leftovers(tuned, algo, mode):
+    """XXH3 and XXH64 descriptor batches of every shape class: 4-16 KiB pages and
     32 KiB pages and 256-byte multiples (one group per page), odd sizes and
     8-byte-aligned offsets (generic lanes), runs of one size, a zero-length
     and a 7-byte page, and pages out of offset order.  Every page must match
@@ -125,28 +128,28 @@ def test_desc_mixed_with_leftovers(tuned, mode):
     host = base.cpu().numpy()
 
     def want_of(h):
-        return np.array([oracle.pages_digest(h[int(a):int(a) + int(L)], int(L), 0)[0] if L >= 8 else 0
+        return np.array([oracle.pages_digest(h[int(a):int(a) + int(L)], int(L), algo)[0] if L >= 8 else 0
                          for a, L in zip(offs, sizes)], dtype=np.uint64)
 
     want = want_of(host)
     if mode == "digest":
-        got = pcs.desc_digest(base, d_off, d_len, n, 0).cpu().numpy().view(np.uint64)
+        got = pcs.desc_digest(base, d_off, d_len, n, algo).cpu().numpy().view(np.uint64)
         assert np.array_equal(got, want), (tuned, np.flatnonzero(got != want)[:8])
     elif mode == "stamp":
-        pcs.desc_stamp(base, d_off, d_len, n, 0)
+        pcs.desc_stamp(base, d_off, d_len, n, algo)
         h2 = base.cpu().numpy()
         for a, L, wv in zip(offs, sizes, want):
             if L >= 8:
                 assert h2[int(a):int(a) + 8].view(np.uint64)[0] == wv
     else:
-        pcs.desc_stamp(base, d_off, d_len, n, 0)
-        ok, fb = pcs.desc_validate(base, d_off, d_len, n, 0)
+        pcs.desc_stamp(base, d_off, d_len, n, algo)
+        ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
         okh = ok.cpu().numpy()
         assert np.array_equal(okh, (sizes >= 8).astype(np.uint8)), tuned
         bad = [i for i in range(5, n, 11) if sizes[i] >= 16]
         flip = torch.from_numpy((offs[bad] + 10).astype(np.int64)).to(DEV)
         base[flip] ^= 0x5A
-        ok, fb = pcs.desc_validate(base, d_off, d_len, n, 0)
+        ok, fb = pcs.desc_validate(base, d_off, d_len, n, algo)
         expect_bad = sorted(set(bad) | set(np.flatnonzero(sizes < 8).tolist()))
         assert np.array_equal(np.flatnonzero(ok.cpu().numpy() == 0), expect_bad), tuned
         assert int(fb.cpu().numpy().view(np.uint64)[0]) == expect_bad[0]
