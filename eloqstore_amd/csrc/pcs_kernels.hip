@@ -657,15 +657,18 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_runs(const uint8_t* __restri
         }
         __builtin_amdgcn_wave_barrier();
         // ---- loader cursors (quads 4ii + r) and the hasher's page ----
+        // (page offsets, not pointers: a pointer that may be null is generic
+        // to the compiler, and flat loads share lgkmcnt with the LDS traffic,
+        // which serialised every segment: 2x slower)
         int lp[4];                // page lane, -1 when the run is done
         uint32_t lo[4], ll[4];    // offset in the page, page length
-        const uint8_t* lptr[4];   // page address
+        uint64_t lb[4];           // page offset from base
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
             lp[ii] = s_first[wv][4 * ii + r];
             lo[ii] = 0;
             ll[ii] = lp[ii] >= 0 ? s_len[wv][lp[ii]] : 0;
-            lptr[ii] = lp[ii] >= 0 ? base + s_off[wv][lp[ii]] : nullptr;
+            lb[ii] = lp[ii] >= 0 ? s_off[wv][lp[ii]] : 0;
         }
         int hp = s_first[wv][hq];
         uint32_t K = hp >= 0 ? s_len[wv][hp] / 64 : 0;
@@ -681,13 +684,13 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_runs(const uint8_t* __restri
                 for (int ii = 0; ii < 4; ++ii) {
                     have[j][ii] = lp[ii] >= 0;
                     if (have[j][ii]) {
-                        d[j][ii] = ld16<NT>(reinterpret_cast<const u32x4*>(lptr[ii] + lo[ii]) + t);
+                        d[j][ii] = ld16<NT>(reinterpret_cast<const u32x4*>(base + lb[ii] + lo[ii]) + t);
                         lo[ii] += 256;
                         if (lo[ii] >= ll[ii]) {  // the run's next page
                             lp[ii] = s_next[wv][lp[ii]];
                             lo[ii] = 0;
                             ll[ii] = lp[ii] >= 0 ? s_len[wv][lp[ii]] : 0;
-                            lptr[ii] = lp[ii] >= 0 ? base + s_off[wv][lp[ii]] : nullptr;
+                            lb[ii] = lp[ii] >= 0 ? s_off[wv][lp[ii]] : 0;
                         }
                     }
                 }
@@ -1902,13 +1905,23 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             const uint64_t id = next_call_id();
             const bool runs = g_tune[29].load(std::memory_order_relaxed) != 0;
             if (runs) {
+                // segments in flight per step from PCS_TUNE_XXH64_LAYOUT, as for k_xxh64_lds
                 const unsigned grid = page_grid(n, 256, 2);
-                if (use_nt())
-                    hipLaunchKernelGGL((k_xxh64_runs<MODE, true, kX64LdsDepth>), dim3(grid), dim3(256), 0, s, base,
-                                       off, len, n, out, ok, fb, word, id);
-                else
-                    hipLaunchKernelGGL((k_xxh64_runs<MODE, false, kX64LdsDepth>), dim3(grid), dim3(256), 0, s, base,
-                                       off, len, n, out, ok, fb, word, id);
+                const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
+                const int depth = lay == 2 ? 1 : lay == 4 ? 4 : 2;
+#define RL(NT_, D_)                                                                                               \
+    hipLaunchKernelGGL((k_xxh64_runs<MODE, NT_, D_>), dim3(grid), dim3(256), 0, s, base, off, len, n, out, ok, fb, \
+                       word, id)
+                if (use_nt()) {
+                    if (depth == 1) RL(true, 1);
+                    else if (depth == 4) RL(true, 4);
+                    else RL(true, 2);
+                } else {
+                    if (depth == 1) RL(false, 1);
+                    else if (depth == 4) RL(false, 4);
+                    else RL(false, 2);
+                }
+#undef RL
             } else {
                 const unsigned grid = page_grid(n, kBlock / 4, 2);
                 if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, word, id);
