@@ -4,9 +4,11 @@
 // compute entry point must fail loudly with PCS_ERR_NO_DEVICE and every
 // argument check must run clean under the sanitizers: null pointers, page
 // sizes, flags, shard ranges at the uint64 edge, tuning keys, batch handles,
-// the skip_verify path (kv_options.h:41) that completes without a device, and
-// the thread-local last-error string.
+// the skip_verify path (kv_options.h:41) that completes without a device, the
+// thread-local last-error string, and the ABI 4 additions (service lines,
+// injected failures, the Try forms and a ChecksumBatch that could not be made).
 #include "eloqstore_pcs.h"
+#include "eloqstore/page_checksum.h"
 
 #include <cstdint>
 #include <cstdio>
@@ -174,11 +176,59 @@ static void last_error_threads() {
     for (int t = 0; t < 8; ++t) CHECK(good[t] == 200);
 }
 
+// ABI 4 additions without a device: pcs_abi_version, pcs_service_start_ex's
+// argument checks (made before the device is looked up), PCS_TUNE_FAIL_INJECT
+// (consumed by the next k host-batch calls, never by skip_verify), and the
+// non-aborting C++ forms the INTEGRATION.md §6 fallback is built on
+static void abi4_no_device() {
+    CHECK(pcs_abi_version() == PCS_ABI_VERSION && PCS_ABI_VERSION >= 4);
+    CHECK(pcs_service_start_ex(0, 4, 0) == PCS_ERR_INVALID);
+    CHECK(std::strstr(pcs_last_error(), "lines must be") != nullptr);
+    CHECK(pcs_service_start_ex(9, 1, 0) == PCS_ERR_INVALID);
+    CHECK(pcs_service_start_ex(8, 33, 0) == PCS_ERR_INVALID);
+    CHECK(std::strstr(pcs_last_error(), "workgroups must be") != nullptr);
+    CHECK(pcs_service_start_ex(2, 0, 0) == PCS_ERR_INVALID);
+    CHECK(pcs_service_start_ex(2, 4, 150) == PCS_ERR_INVALID);
+    CHECK(pcs_service_start_ex(8, 32, 0) == PCS_ERR_NO_DEVICE);  // 256 workgroups: arguments fine
+    CHECK(pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS) == 0);
+    CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_MAX_CALLERS) == 2 && pcs_get_tuning(PCS_TUNE_XXH64_RUNS) == 0);
+    CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && pcs_get_tuning(PCS_TUNE_SERVICE_TEAR_TEST) == 0);
+
+    std::vector<char> page(4096, 0x33);
+    const char* cpages[1] = {page.data()};
+    char* wpages[1] = {page.data()};
+    uint8_t ok[1] = {7};
+    size_t fb = 99;
+    CHECK(pcs_set_tuning(PCS_TUNE_FAIL_INJECT, 2) == PCS_OK);
+    // skip_verify never reaches the GPU and leaves the injections alone
+    CHECK(eloqstore::TryValidateChecksums(cpages, 4096, ok, &fb, eloqstore::PageHash::XXH3_64, true) == PCS_OK);
+    CHECK(ok[0] == 1 && fb == 1 && pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 2);
+    fb = 99;
+    CHECK(eloqstore::TryValidateChecksums(cpages, 4096, ok, &fb) == PCS_ERR_HIP && fb == 99);
+    CHECK(std::strstr(eloqstore::LastChecksumError(), "injected failure") != nullptr);
+    CHECK(eloqstore::TrySetChecksums(wpages, 4096) == PCS_ERR_HIP);
+    CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && page[0] == 0x33);
+    // injections spent: the plain no-device failure again
+    CHECK(eloqstore::TryValidateChecksums(cpages, 4096, ok, &fb) == PCS_ERR_NO_DEVICE);
+    CHECK(std::strstr(eloqstore::LastChecksumError(), "no usable HIP device") != nullptr);
+    CHECK(eloqstore::TrySetChecksums(wpages, 4096, eloqstore::PageHash::XXH64) == PCS_ERR_NO_DEVICE);
+    CHECK(pcs_set_tuning(PCS_TUNE_FAIL_INJECT, -1) == PCS_ERR_INVALID);
+
+    // a batch that could not be created reports why on every call, never aborts
+    eloqstore::ChecksumBatch cb;
+    CHECK(cb.Status() == PCS_ERR_NO_DEVICE);
+    CHECK(cb.TrySubmitValidate(cpages, 4096) == PCS_ERR_NO_DEVICE);
+    CHECK(cb.TrySubmitValidate(cpages, 4096, eloqstore::PageHash::XXH3_64, true) == PCS_ERR_NO_DEVICE);
+    CHECK(cb.TrySubmitStamp(wpages, 4096) == PCS_ERR_NO_DEVICE);
+    CHECK(cb.TryPoll() == PCS_ERR_NO_DEVICE);
+}
+
 int main() {
     shard_ranges();
     no_device();
     arguments();
     last_error_threads();
+    abi4_no_device();
     if (g_fail) {
         std::fprintf(stderr, "%d check(s) failed\n", g_fail);
         return 1;
