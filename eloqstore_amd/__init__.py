@@ -162,7 +162,6 @@ TUNE_SERVICE_STREAM = 24
 TUNE_SERVICE_TEAR_TEST = 26  # test only
 TUNE_FAIL_INJECT = 27  # test only
 TUNE_SERVICE_MAX_CALLERS = 28
-TUNE_XXH64_RUNS = 29
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

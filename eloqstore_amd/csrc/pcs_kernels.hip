@@ -553,203 +553,6 @@ __global__ __launch_bounds__(64 * WPB) void k_xxh64_lds(const uint8_t* __restric
     }
 }
 
-// XXH64 descriptor pages as equal-byte runs (PCS_TUNE_XXH64_RUNS).
-//
-// k_xxh64_lds gives each quad of a wave one page, so a wave walks its longest
-// page while the quads with shorter ones idle: on config 3 (4/8/16 KiB mixed)
-// only ~58 % of the lane slots have bytes to fetch, and the L2 has 241 reads
-// in flight against 421 on uniform pages.  Here a wave takes
-// a window of 64 consecutive descriptors and cuts it into 16 runs of
-// consecutive pages with about equal bytes (run = floor(16 * bytes before the
-// page / window bytes)); quad q hashes run q's pages one after another,
-// finalising each at its last chunk.  Address order is kept (each run is a
-// contiguous slice of the window), and every quad walks about the same bytes.
-// Loads keep k_xxh64_lds's row pattern and LDS hand-off (row r of the wave
-// loads the next 256-byte segment of quads 4ii + r).  Pages must be runs-
-// shaped (length a multiple of 256, >= 256, 16-byte-aligned offset: every
-// power-of-two page size); others go to the generic lanes (flagged like
-// k_xxh64_lds's off-shape pages, FILTER 3 there).
-__device__ __forceinline__ bool xxh64_runs_ok(uint64_t off, uint32_t P) {
-    return (P % 256u) == 0 && P >= 256u && (off % 16u) == 0;
-}
-
-template <int MODE, bool NT, int DEPTH, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) void k_xxh64_runs(const uint8_t* __restrict__ base,
-                                                        const uint64_t* __restrict__ off,
-                                                        const uint32_t* __restrict__ len, uint64_t n,
-                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                        unsigned long long* first_bad, unsigned long long* offshape,
-                                                        uint64_t call_id) {
-    __shared__ __attribute__((aligned(16))) u32x4 lds[WPB][16][16];  // [wave][quad][16 B slot]
-    __shared__ uint64_t s_off[WPB][64];
-    __shared__ uint32_t s_len[WPB][64];
-    __shared__ int8_t s_next[WPB][64];   // next page lane of the same run, or -1
-    __shared__ int8_t s_first[WPB][16];  // first page lane of run q, or -1
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int r = lane >> 4, t = lane & 15;        // loader role
-    const int i = (lane >> 2) & 3, q = lane & 3;   // hasher role: quad 4i + r, quad lane q
-    const int a = q == 2 ? 3 : q == 3 ? 2 : q;
-    const int hq = 4 * i + r;                      // this lane's hasher quad (its run)
-    constexpr uint64_t kTile = 64 * WPB;
-    const uint64_t ntiles = (n + kTile - 1) / kTile;
-    const bool remap = gridDim.x == ntiles;
-    for (uint64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-        const uint64_t W0 = (remap ? xcd_tile_eighths(t0, ntiles) : t0) * kTile + (uint64_t)wv * 64;
-        // ---- the window's page table and its cut into 16 runs ----
-        const uint64_t pg = W0 + lane;
-        uint64_t o = 0;
-        uint32_t L = 0;
-        bool elig = false;
-        if (pg < n) {
-            o = off[pg];
-            L = len[pg];
-            elig = xxh64_runs_ok(o, L);
-            if (!elig && offshape) *offshape = call_id;  // left to k_generic_desc: it must run
-        }
-        const uint64_t b = elig ? L : 0;
-        uint64_t incl = b;  // inclusive prefix sum of run bytes over the wave
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t x = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += x;
-        }
-        const uint64_t total = __shfl(incl, 63, 64);
-        const uint64_t excl = incl - b;
-        const uint64_t cut = excl * 16 / (total ? total : 1);
-        const int run = elig ? (int)(cut < 15 ? cut : 15) : -1;
-        const uint64_t emask = __ballot(elig);
-        // next eligible lane after this one, and whether it is in the same run
-        const uint64_t above = lane == 63 ? 0 : (emask >> (lane + 1)) << (lane + 1);
-        const int nxt = above ? __builtin_ctzll(above) : -1;
-        const int run_nxt = __shfl(run, nxt < 0 ? lane : nxt, 64);
-        const uint64_t below = lane == 0 ? 0 : emask & ((1ull << lane) - 1);
-        const int prv = below ? 63 - __builtin_clzll(below) : -1;
-        const int run_prv = __shfl(run, prv < 0 ? lane : prv, 64);
-        if (lane < 16) s_first[wv][lane] = -1;
-        __builtin_amdgcn_wave_barrier();
-        s_off[wv][lane] = o;
-        s_len[wv][lane] = L;
-        s_next[wv][lane] = (int8_t)(elig && nxt >= 0 && run_nxt == run ? nxt : -1);
-        if (elig && (prv < 0 || run_prv != run)) s_first[wv][run] = (int8_t)lane;
-        // run bytes: last page of a run has incl = end, first has excl = start
-        uint32_t segs_mine = 0;
-        {
-            // each lane that ends a run publishes its run's segment count
-            const bool ends = elig && (nxt < 0 || run_nxt != run);
-            uint64_t start = excl;
-            // the run's start = excl of its first lane: walk back via shfl is
-            // costly; instead every lane of the run carries excl of the first
-            // lane through a max-scan of "start if first else 0"
-            const bool first = elig && (prv < 0 || run_prv != run);
-            uint64_t st = first ? excl + 1 : 0;  // +1: 0 means "none"
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint64_t x = __shfl_up(st, d, 64);
-                if (lane >= d && x > st) st = x;
-            }
-            start = st ? st - 1 : 0;
-            if (ends) segs_mine = (uint32_t)((incl - start) / 256);
-        }
-        uint32_t segs = segs_mine;
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t x = (uint32_t)__shfl_xor((int)segs, d, 64);
-            segs = x > segs ? x : segs;
-        }
-        __builtin_amdgcn_wave_barrier();
-        // ---- loader cursors (quads 4ii + r) and the hasher's page ----
-        // (page offsets, not pointers: a pointer that may be null is generic
-        // to the compiler, and flat loads share lgkmcnt with the LDS traffic,
-        // which serialised every segment: 2x slower)
-        int lp[4];                // page lane, -1 when the run is done
-        uint32_t lo[4], ll[4];    // offset in the page, page length
-        uint64_t lb[4];           // page offset from base
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-            lp[ii] = s_first[wv][4 * ii + r];
-            lo[ii] = 0;
-            ll[ii] = lp[ii] >= 0 ? s_len[wv][lp[ii]] : 0;
-            lb[ii] = lp[ii] >= 0 ? s_off[wv][lp[ii]] : 0;
-        }
-        int hp = s_first[wv][hq];
-        uint32_t K = hp >= 0 ? s_len[wv][hp] / 64 : 0;
-        uint32_t kk = 0;
-        uint64_t v = xxh64_init(a), stored = 0;
-        u32x4 last = {0, 0, 0, 0};
-        for (uint32_t c0 = 0; c0 < segs; c0 += DEPTH) {
-            u32x4 d[DEPTH][4];
-            bool have[DEPTH][4];
-#pragma unroll
-            for (int j = 0; j < DEPTH; ++j)
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii) {
-                    have[j][ii] = lp[ii] >= 0;
-                    if (have[j][ii]) {
-                        d[j][ii] = ld16<NT>(reinterpret_cast<const u32x4*>(base + lb[ii] + lo[ii]) + t);
-                        lo[ii] += 256;
-                        if (lo[ii] >= ll[ii]) {  // the run's next page
-                            lp[ii] = s_next[wv][lp[ii]];
-                            lo[ii] = 0;
-                            ll[ii] = lp[ii] >= 0 ? s_len[wv][lp[ii]] : 0;
-                            lb[ii] = lp[ii] >= 0 ? s_off[wv][lp[ii]] : 0;
-                        }
-                    }
-                }
-#pragma unroll
-            for (int j = 0; j < DEPTH; ++j) {
-                if (c0 + j >= segs) break;  // wave-uniform
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii)
-                    if (have[j][ii]) lds[wv][4 * ii + r][(t + 4 * ii) & 15] = d[j][ii];
-                __builtin_amdgcn_wave_barrier();
-                if (hp >= 0) {  // quad-uniform
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const u32x4 e = lds[wv][hq][(4 * k + q + 4 * i) & 15];
-                        if (kk == 0) stored = dpp64<quad_bcast(0)>(lo64(e));
-                        if (kk == 0 || kk == K - 1)
-                            xxh64_chunk<true>(v, e, q, q == 2 && kk == 0, q != 2 && kk == K - 1);
-                        else xxh64_chunk<false>(v, e, q, false, false);
-                        if (kk == K - 1) last = e;
-                        ++kk;
-                    }
-                    if (kk == K) {  // the page's last chunk: finalise, emit, next page of the run
-                        const uint64_t v0 = dpp64<quad_bcast(0)>(v);
-                        const uint64_t v1 = dpp64<quad_bcast(1)>(v);
-                        const uint64_t v2 = dpp64<quad_bcast(3)>(v);
-                        const uint64_t v3 = dpp64<quad_bcast(2)>(v);
-                        uint64_t h = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
-                        h = (h ^ xxh64_round(0, v0)) * kP64_1 + kP64_4;
-                        h = (h ^ xxh64_round(0, v1)) * kP64_1 + kP64_4;
-                        h = (h ^ xxh64_round(0, v2)) * kP64_1 + kP64_4;
-                        h = (h ^ xxh64_round(0, v3)) * kP64_1 + kP64_4;
-                        const uint32_t Ph = s_len[wv][hp];
-                        h += (uint64_t)(Ph - 8);
-                        const uint64_t t0w = dpp64<quad_bcast(2)>(hi64(last));
-                        const uint64_t t1w = dpp64<quad_bcast(3)>(lo64(last));
-                        const uint64_t t2w = dpp64<quad_bcast(3)>(hi64(last));
-                        h ^= xxh64_round(0, t0w);
-                        h = rotl64(h, 27) * kP64_1 + kP64_4;
-                        h ^= xxh64_round(0, t1w);
-                        h = rotl64(h, 27) * kP64_1 + kP64_4;
-                        h ^= xxh64_round(0, t2w);
-                        h = rotl64(h, 27) * kP64_1 + kP64_4;
-                        h = xxh64_avalanche(h);
-                        if (q == 0)
-                            emit(MODE, W0 + hp, h, stored, const_cast<uint8_t*>(base + s_off[wv][hp]), out, ok,
-                                 first_bad);
-                        hp = s_next[wv][hp];
-                        K = hp >= 0 ? s_len[wv][hp] / 64 : 0;
-                        kk = 0;
-                        v = xxh64_init(a);
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // the page table is rewritten by the next window
-    }
-}
-
 // Pages off the 64-byte-piece shape (P % 64 != 0 or 8-byte-aligned only): one
 // quad per page, lane a reading accumulator a's words (xxh64_page).  The quad
 // layout for line-shaped pages (each quad loading its own 64 B pieces, 80 % of
@@ -1031,7 +834,6 @@ __global__ __launch_bounds__(256) void k_generic_desc(const uint8_t* __restrict_
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (filter == 1 && algo == 1 && xxh64_lines_ok(off[i], len[i])) continue;
-        if (filter == 3 && algo == 1 && xxh64_runs_ok(off[i], len[i])) continue;
         if (filter == 2 && xxh3_long_ok(base + off[i], len[i])) continue;
         generic_one<MODE>(base, off, len, i, algo, seed, skip, out, ok, first_bad);
     }
@@ -1616,7 +1418,7 @@ constexpr int kTuneKeys = 30;
 // knob in commit 01e849b).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, true,  false, false, false, false};
+                                      false, true,  false, false, false, true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1637,7 +1439,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*test only: validate service torn-line drill, microseconds*/ 0,
                                           /*test only: host-batch calls left to fail*/ 0,
                                           /*validate service contention gate: callers (0 = off)*/ 2,
-                                          /*XXH64 descriptor pages as equal-byte runs per quad (k_xxh64_runs)*/ 0};
+                                          /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1903,30 +1705,9 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             if (e != hipSuccess) return e;
             auto* word = static_cast<unsigned long long*>(flag.p);
             const uint64_t id = next_call_id();
-            const bool runs = g_tune[29].load(std::memory_order_relaxed) != 0;
-            if (runs) {
-                // segments in flight per step from PCS_TUNE_XXH64_LAYOUT, as for k_xxh64_lds
-                const unsigned grid = page_grid(n, 256, 2);
-                const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
-                const int depth = lay == 2 ? 1 : lay == 4 ? 4 : 2;
-#define RL(NT_, D_)                                                                                               \
-    hipLaunchKernelGGL((k_xxh64_runs<MODE, NT_, D_>), dim3(grid), dim3(256), 0, s, base, off, len, n, out, ok, fb, \
-                       word, id)
-                if (use_nt()) {
-                    if (depth == 1) RL(true, 1);
-                    else if (depth == 4) RL(true, 4);
-                    else RL(true, 2);
-                } else {
-                    if (depth == 1) RL(false, 1);
-                    else if (depth == 4) RL(false, 4);
-                    else RL(false, 2);
-                }
-#undef RL
-            } else {
-                const unsigned grid = page_grid(n, kBlock / 4, 2);
-                if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, word, id);
-                else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, word, id);
-            }
+            const unsigned grid = page_grid(n, kBlock / 4, 2);
+            if (use_nt()) launch_xxh64_lds<MODE, true, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, word, id);
+            else launch_xxh64_lds<MODE, false, kAddrDesc>(grid, s, base, off, len, 0u, n, out, ok, fb, word, id);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
             // one block per CU: when every page conforms (the usual case)
@@ -1935,7 +1716,7 @@ static hipError_t desc_impl(int algo, const uint8_t* base, const uint64_t* off, 
             // off-shape pages take the grid-stride loop
             const unsigned ggrid = std::min(grid_for(n, kBlock, kBlocksPerCu), (unsigned)cu_count());
             hipLaunchKernelGGL((k_generic_desc<MODE>), dim3(ggrid), dim3(kBlock), 0, s, base, off, len, n, algo, seed,
-                               skip, runs ? 3 : 1, out, ok, fb, word, id);
+                               skip, 1, out, ok, fb, word, id);
             return hipGetLastError();
         }
     }

@@ -304,11 +304,6 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     this + lines - 1 + 0.5, the service
  *                                     declines and calls take the launch
  *                                     path; 0 = off
- *   PCS_TUNE_XXH64_RUNS           [0] XXH64 descriptor batches: 1 = each wave
- *                                     cuts a window of 64 pages into 16
- *                                     equal-byte runs, one quad hashing each
- *                                     run (pages of a multiple of 256 bytes);
- *                                     0 = one page per quad (k_xxh64_lds)
  *   PCS_TUNE_SERVICE_TEAR_TEST    [0] test only: microseconds the service's
  *                                     host side waits between posting seq and
  *                                     writing the request words (the kernel
@@ -318,12 +313,12 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     pcs_batch_poll / wait,
  *                                     pcs_manifest_*_host) fail with
  *                                     PCS_ERR_HIP; decremented per failure
- * Keys 4, 5, 10, 12, 14, 16-22 and 25 selected variants that measured slower or no
+ * Keys 4, 5, 10, 12, 14, 16-22, 25 and 29 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
  * tiles, plain result stores, 4 KiB-aligned descriptor steps, a 4-waves-
  * per-SIMD descriptor body; round 3: an XXH64 direct-to-LDS segment ring,
- * XXH64 tile-order chunks);
+ * XXH64 tile-order chunks; round 4: XXH64 equal-byte runs per quad);
  * they were retired: setting one fails and reading one
  * returns -1. */
 enum pcs_tune_key {
@@ -342,7 +337,6 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_TEAR_TEST = 26,
     PCS_TUNE_FAIL_INJECT = 27,
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
-    PCS_TUNE_XXH64_RUNS = 29,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -191,7 +191,7 @@ static void abi4_no_device() {
     CHECK(pcs_service_start_ex(2, 4, 150) == PCS_ERR_INVALID);
     CHECK(pcs_service_start_ex(8, 32, 0) == PCS_ERR_NO_DEVICE);  // 256 workgroups: arguments fine
     CHECK(pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS) == 0);
-    CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_MAX_CALLERS) == 2 && pcs_get_tuning(PCS_TUNE_XXH64_RUNS) == 0);
+    CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_MAX_CALLERS) == 2 && pcs_get_tuning(29) == -1);
     CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && pcs_get_tuning(PCS_TUNE_SERVICE_TEAR_TEST) == 0);
 
     std::vector<char> page(4096, 0x33);

@@ -29,8 +29,6 @@ VARIANTS = {
     "split_64k": {pcs.TUNE_XXH3_SPLIT_PAGES: 65536},
     "x64_one_wave": {pcs.TUNE_XXH64_WAVES: 1},
     "x64_two_waves_depth4": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 4},
-    "x64_runs": {pcs.TUNE_XXH64_RUNS: 1},
-    "x64_runs_no_nt": {pcs.TUNE_XXH64_RUNS: 1, pcs.TUNE_NT_LOADS: 0},
 }
 
 
@@ -68,7 +66,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_one_wave",
-                                   "x64_two_waves_depth4", "x64_runs", "x64_runs_no_nt"],
+                                   "x64_two_waves_depth4"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):
@@ -97,8 +95,7 @@ def test_variant_mixed_desc(tuned, algo):
     assert int(fb.cpu().numpy().view(np.uint64)[0]) == 3
 
 
-@pytest.mark.parametrize("tuned,algo", [("default", 0), ("no_nt", 0), ("rt_one_block", 0), ("default", 1),
-                                        ("x64_runs", 1), ("x64_runs_no_nt", 1)], indirect=["tuned"])
+@pytest.mark.parametrize("tuned,algo", [("default", 0), ("no_nt", 0), ("rt_one_block", 0), ("default", 1)], indirect=["tuned"])
 @pytest.mark.parametrize("mode", ["digest", "validate", "stamp"])
 def test_desc_mixed_with_leftovers(tuned, algo, mode):
     """XXH3 and XXH64 descriptor batches of every shape class: 4-16 KiB pages and
