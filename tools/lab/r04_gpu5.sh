@@ -1,6 +1,8 @@
 # XXH64 equal-byte runs (PCS_TUNE_XXH64_RUNS): parity first, then an
 # interleaved A/B against k_xxh64_lds on config 3 (digest, validate, stamp),
 # runs at depths 1 / 2 / 4 (PCS_TUNE_XXH64_LAYOUT 2 / 0 / 4).
+# Result: profiles/r04/x64_runs_ab.txt (runs 18-28 % slower); the kernel and
+# key 29 were retired after it (commit 473b0b4), so this reruns only at 9196877.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r04g
