@@ -44,8 +44,10 @@ Also reported, on the same line:
                 config 2 validate (read path) and stamp (write path), each with
                 its avg launch time, roofline frac, parity sample and
                 corruption drill.
-  scaling       (N>1) per-rank wall and kernel-event times, and efficiency =
-                per-GPU rate / rank 0's rate on the same shard run alone.
+  scaling_detail (N>1) per-rank wall and kernel-event times, and
+                concurrent_over_solo = per-GPU rate / rank 0's rate on the same
+                shard run alone (an interference check; scaling efficiency is
+                the driver's, from the per-N values).
 """
 from __future__ import annotations
 
@@ -852,7 +854,8 @@ def main():
     scaling = None
     if dist is not None:
         # Per-rank evidence, then rank 0 alone on its own shard (the others wait
-        # at the barrier): efficiency = concurrent per-GPU rate / solo rate.
+        # at the barrier): concurrent per-GPU rate / solo rate, an interference
+        # check (the driver computes scaling efficiency from the per-N lines).
         per_rank = [None] * world
         dist.all_gather_object(per_rank, {"rank": rank, "gpu": gpu, "wall_s": round(t1 - t0, 5),
                                           "kernel_event_ms_per_step": round(avg_launch * 1e3, 4),
@@ -869,9 +872,9 @@ def main():
         barrier(dist)
         if rank == 0:
             scaling = {"per_rank": per_rank, "solo_rank0_GiBps": round(solo, 1),
-                       "efficiency": round(value / world / solo, 4),
-                       "efficiency_def": "per-GPU rate of the concurrent run / rank 0's rate on the same shard "
-                                         "run alone in this job",
+                       "concurrent_over_solo": round(value / world / solo, 4),
+                       "concurrent_over_solo_def": "per-GPU rate of the concurrent run / rank 0's rate on the "
+                                                   "same shard run alone in this job",
                        "shared_gpus": ndev < world}
         time.sleep(PHASE_GAP_S)
 

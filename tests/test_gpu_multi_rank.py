@@ -79,7 +79,7 @@ def test_bench_two_ranks_torchrun():
     """The driver's scaling launch, rehearsed with 2 ranks on the box's one GPU:
     with no --config, N>1 defaults to BASELINE config 5 (8 M x 4 KiB pages =
     32 GiB per rank, generated in place); rank 0 prints one line with per-rank
-    wall/kernel-event times and the efficiency against its solo rate."""
+    wall/kernel-event times and the concurrent rate against its solo rate."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1"]
@@ -96,5 +96,5 @@ def test_bench_two_ranks_torchrun():
     sd = line["scaling_detail"]
     assert [p["rank"] for p in sd["per_rank"]] == [0, 1]
     assert all(p["kernel_event_ms_per_step"] > 0 and p["wall_s"] > 0 for p in sd["per_rank"])
-    assert sd["efficiency"] > 0 and sd["solo_rank0_GiBps"] > 0 and sd["shared_gpus"]
+    assert sd["concurrent_over_solo"] > 0 and sd["solo_rank0_GiBps"] > 0 and sd["shared_gpus"]
     assert "sweep" not in line  # the sweep is an N=1 leg
