@@ -873,7 +873,8 @@ int service_progress(ServiceReq& r) {
         std::atomic_thread_fence(std::memory_order_acquire);
         return 1;
     }
-    if (sv.device < 0 || ++r.relaunched > 3) return kFallback;
+    // (a restart with fewer lines serves no workgroup on this one)
+    if (sv.device < 0 || r.k >= sv.lines || ++r.relaunched > 3) return kFallback;
     if (r.gen == sv.gen.load(std::memory_order_relaxed) || !service_waiting(sv, r.k, now))
         if (int rc = service_launch_locked(sv)) {
             (void)service_reset_locked(sv);

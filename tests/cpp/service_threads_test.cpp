@@ -18,6 +18,15 @@
 //   5. four request lines (pcs_service_start_ex): eight threads exact with
 //      the gate off, four threads served on most calls with it on.
 // The CPU oracle is the checker.  Prints "service threads ok" on success.
+//
+// --soak SECONDS runs only the soak instead: eight threads mix sync
+// validates, async validates and stamps of their own pages (every validate
+// with a corrupted page, every stamp over a zeroed header) while a controller
+// thread keeps changing the service under them: stop, restart with 1-8 lines
+// of 1-4 workgroups and another idle time, gate knob 0/2/4, short torn-line
+// drills.  Every result must be exact on whichever path served it; prints
+// the path mix, restarts and latency percentiles, then "service soak ok".
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -116,9 +125,126 @@ int run_validate(char* pool, int T, double secs, bool async, size_t max_n, std::
     for (auto& x : th) x.join();
     return errors.load();
 }
+// --soak: see the header
+int soak(char* pool, int T, double secs) {
+    std::atomic<int> errors{0};
+    std::atomic<bool> done{false};
+    std::atomic<uint64_t> n_sync{0}, n_async{0}, n_stamp{0};
+    std::vector<std::vector<float>> lat(T);
+    const Counts c0 = counts();
+    const uint64_t torn0 = pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS);
+    CHECK(pcs_service_start_ex(2, 2, 0) == PCS_OK);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            uint64_t rng = 0x50A4ull + t * 104729ull;
+            eloqstore::ChecksumBatch cb;
+            std::vector<uint8_t> ok;
+            while (!done.load(std::memory_order_relaxed)) {
+                const int op = (int)(splitmix(rng) % 3);
+                Req r = make_req(pool, t, rng, splitmix(rng) % 4 ? 24 : 256);
+                const auto t0 = Clock::now();
+                bool good = true;
+                if (op == 2) {  // stamp over zeroed headers
+                    std::vector<char*> w;
+                    for (const char* p : r.ptrs) {
+                        w.push_back(const_cast<char*>(p));
+                        std::memset(w.back(), 0, 8);
+                    }
+                    eloqstore::SetChecksums(w, P);
+                    for (char* p : w) {
+                        uint64_t hdr;
+                        std::memcpy(&hdr, p, 8);
+                        good &= hdr == oracle_page_xxh3(p, P);
+                    }
+                    n_stamp.fetch_add(1, std::memory_order_relaxed);
+                } else {
+                    char* bad = const_cast<char*>(r.ptrs[r.k]);
+                    bad[r.byte] ^= 0x04;
+                    size_t fb;
+                    const uint8_t* v;
+                    if (op == 1) {
+                        cb.SubmitValidate(r.ptrs, P);
+                        while (!cb.Poll()) {
+                        }
+                        fb = cb.FirstBad();
+                        v = cb.Verdicts();
+                        n_async.fetch_add(1, std::memory_order_relaxed);
+                    } else {
+                        ok.assign(r.ptrs.size(), 9);
+                        fb = eloqstore::ValidateChecksums(r.ptrs, P, ok.data());
+                        v = ok.data();
+                        n_sync.fetch_add(1, std::memory_order_relaxed);
+                    }
+                    bad[r.byte] ^= 0x04;
+                    good = fb == r.k;
+                    for (size_t i = 0; i < r.ptrs.size(); ++i) good &= v[i] == (i != r.k);
+                }
+                lat[t].push_back(std::chrono::duration<float, std::micro>(Clock::now() - t0).count());
+                if (!good && errors.fetch_add(1) < 5)
+                    std::fprintf(stderr, "soak thread %d: op %d n %zu slot %zu wrong\n", t, op, r.ptrs.size(), r.k);
+            }
+        });
+    // the controller
+    uint64_t rng = 0xC7A1ull;
+    int restarts = 0, gates = 0, drills = 0, stopped_ms = 0;
+    const auto end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(secs));
+    while (Clock::now() < end) {
+        std::this_thread::sleep_for(std::chrono::microseconds(2000 + splitmix(rng) % 18000));
+        switch (splitmix(rng) % 4) {
+        case 0: {  // restart with another shape
+            CHECK(pcs_service_stop() == PCS_OK);
+            if (splitmix(rng) % 3 == 0) {  // a stretch with no service at all
+                const int ms = 1 + (int)(splitmix(rng) % 10);
+                std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+                stopped_ms += ms;
+            }
+            const int lines = 1 << (splitmix(rng) % 4), wpl = 1 << (splitmix(rng) % 3);
+            const uint32_t idles[] = {0, 200, 500, 5000};
+            CHECK(pcs_service_start_ex(lines, wpl, idles[splitmix(rng) % 4]) == PCS_OK);
+            ++restarts;
+            break;
+        }
+        case 1:
+        case 2: {
+            const int64_t gate[] = {0, 2, 4};
+            CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, gate[splitmix(rng) % 3]) == PCS_OK);
+            ++gates;
+            break;
+        }
+        default:  // a short torn-line drill under the running threads
+            CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_TEAR_TEST, 20) == PCS_OK);
+            std::this_thread::sleep_for(std::chrono::microseconds(500));
+            CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_TEAR_TEST, 0) == PCS_OK);
+            ++drills;
+        }
+    }
+    done = true;
+    for (auto& x : th) x.join();
+    CHECK(pcs_service_stop() == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
+    const Counts c1 = counts();
+    std::vector<float> all;
+    for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+    std::sort(all.begin(), all.end());
+    auto pct = [&](double q) { return all.empty() ? 0.f : all[std::min(all.size() - 1, (size_t)(q * all.size()))]; };
+    const uint64_t total = n_sync + n_async + n_stamp;
+    std::printf("soak %.0f s, %d threads: %llu requests exact (%llu sync validate, %llu async validate, %llu stamp; "
+                "%llu served, %llu launched), %d restarts (%d ms with no service), %d gate changes, %d torn drills "
+                "(%llu torn requests ignored)\n",
+                secs, T, (unsigned long long)total, (unsigned long long)n_sync.load(),
+                (unsigned long long)n_async.load(), (unsigned long long)n_stamp.load(),
+                (unsigned long long)(c1.served - c0.served), (unsigned long long)(c1.launched - c0.launched),
+                restarts, stopped_ms, gates, drills,
+                (unsigned long long)(pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS) - torn0));
+    std::printf("soak latency us: p50 %.1f  p99 %.1f  p99.9 %.1f  max %.1f\n", pct(0.5), pct(0.99), pct(0.999),
+                all.empty() ? 0.f : all.back());
+    CHECK(c1.served > c0.served && c1.launched > c0.launched && restarts > 0);
+    return errors.load();
+}
 }  // namespace
 
-int main() {
+int main(int argc, char** argv) {
     constexpr int T = 8;
     const size_t np = T * PER;
     char* pool = static_cast<char*>(std::aligned_alloc(4096, np * P));
@@ -126,6 +252,13 @@ int main() {
     oracle_fill_pages(pool, P, np, 0x7E57, 0);
     for (size_t i = 0; i < np; ++i) oracle_set_checksum(pool + i * P, P);
     eloqstore::RegisterPagePool(pool, np * P);
+    if (argc == 3 && std::strcmp(argv[1], "--soak") == 0) {
+        CHECK(soak(pool, T, std::atof(argv[2])) == 0);
+        eloqstore::UnregisterPagePool(pool);
+        std::free(pool);
+        std::printf("service soak ok\n");
+        return 0;
+    }
     eloqstore::StartChecksumService(4, 1000);
 
     // 1 + 2: exact verdicts under eight native threads, gate off
