@@ -361,20 +361,6 @@ def test_service_native_threads_and_gate():
     print(r.stdout)
 
 
-def test_service_soak_under_restarts():
-    """tests/cpp/service_threads_test.cpp --soak: eight native threads mix
-    sync validates, async validates and stamps while a controller thread
-    stops and restarts the service with other line / workgroup / idle
-    shapes, flips the gate knob and runs torn-line drills under them: every
-    verdict, first_bad and header exact on whichever path served it."""
-    import os
-    import subprocess
-    exe = os.path.join(os.path.dirname(__file__), "cpp", "service_threads_test")
-    r = subprocess.run([exe, "--soak", "12"], capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0 and "service soak ok" in r.stdout, r.stdout + r.stderr
-    print(r.stdout)
-
-
 def test_service_async_batches(service):
     """ChecksumBatch (pcs_batch_*) validate and stamp batches posted to the
     service: submit returns at once, poll watches the verdict words;
