@@ -162,12 +162,14 @@ TUNE_SERVICE_STREAM = 24
 TUNE_SERVICE_TEAR_TEST = 26  # test only
 TUNE_FAIL_INJECT = 27  # test only
 TUNE_SERVICE_MAX_CALLERS = 28
+TUNE_SERVICE_REPOST_TEST = 30  # test only
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1
 COUNTER_GATHER_CHUNKS = 2
 COUNTER_SERVICE_BATCHES = 3
 COUNTER_SERVICE_TORN_REQUESTS = 4
+COUNTER_SERVICE_REPOSTS = 5
 
 
 def counter(which: int) -> int:
@@ -187,7 +189,7 @@ def version() -> str:
     return lib().pcs_version().decode()
 
 
-ABI_VERSION = 4  # PCS_ABI_VERSION of include/eloqstore_pcs.h this binding was written for
+ABI_VERSION = 5  # PCS_ABI_VERSION of include/eloqstore_pcs.h this binding was written for
 
 
 def abi_version() -> int:

@@ -525,8 +525,14 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // A request is only ever served by the workgroups of its own generation, and
 // it is re-posted under a newer generation only once the kernel of the
 // generation it was posted to has left (an event recorded behind each
-// service kernel says so).  So no workgroup can still be writing a request's
-// verdicts after its owner has read them and released the line.
+// service kernel says so).  A re-post re-arms every verdict word first: the
+// old generation may have answered some pages (with wpl > 1, some of a
+// line's workgroups can leave before picking the request up while others
+// answer it), and the new generation's workgroups hash all of them again.
+// The host then waits for every verdict of the new generation, and a
+// workgroup writes a page's verdict after its last read of the request, so
+// no workgroup can still be reading a request's words or writing its
+// verdicts after its owner has read them and released the line (ADVICE r04).
 //
 // The mailbox is allocated at a device's first start and kept for the life
 // of the process, so an asynchronous request still in flight when the
@@ -614,11 +620,11 @@ uint64_t service_check(const pcs::ServiceLine* ln, uint64_t seq) {
     return c;
 }
 
-// Post the request words already on line k under the current generation: the
-// check word, then seq last.
-uint64_t service_post_locked(Service& sv, int k) {
+// Post the request words already on line k under generation `gen` (the
+// current one but for the re-post drill): the check word, then seq last.
+uint64_t service_post_locked(Service& sv, int k, uint32_t gen) {
     pcs::ServiceLine* ln = &sv.h->line[k];
-    const uint64_t seq = (uint64_t)sv.gen.load(std::memory_order_relaxed) << 32 | ++sv.line[k].count;
+    const uint64_t seq = (uint64_t)gen << 32 | ++sv.line[k].count;
     ln->check = service_check(ln, seq);
     std::atomic_thread_fence(std::memory_order_release);
     __atomic_store_n(&ln->seq, seq, __ATOMIC_RELEASE);
@@ -705,11 +711,22 @@ void caller_enter(Service& sv) {
 }
 void caller_leave(Service& sv) { sv.callers.fetch_sub(1, std::memory_order_relaxed); }
 
-// The calling thread's device's service when it is on (else null), counted
-// as a caller for the guard's lifetime.
+// The shape the service takes (service_submit): XXH3, 1..256 pages, a page
+// size on the 256-byte grid.  Only such calls count as callers, so XXH64,
+// large or odd-size traffic on the launch path cannot close the gate for the
+// small XXH3 batches it exists for.  Whether the pages lie in
+// registered memory is found out later, under the service's lock; such calls
+// are counted.
+bool service_shape_ok(uint64_t P, uint64_t n, int algo) {
+    return algo == PCS_XXH3_64 && n >= 1 && n <= (uint64_t)pcs::kServiceMaxPages && pcs::list_shape_ok(0, P);
+}
+
+// The calling thread's device's service when it is on and the call has the
+// service's shape (else null), counted as a caller for the guard's lifetime.
 class CallerGuard {
 public:
-    explicit CallerGuard(Service* sv) : sv_(sv && sv->device >= 0 ? sv : nullptr) {
+    CallerGuard(Service* sv, uint64_t P, uint64_t n, int algo)
+        : sv_(sv && sv->device >= 0 && service_shape_ok(P, n, algo) ? sv : nullptr) {
         if (sv_) caller_enter(*sv_);
     }
     ~CallerGuard() {
@@ -728,7 +745,7 @@ private:
 // paths (a flapping gate relaunches the idled-out kernel again and again:
 // p99 54.7 µs at 4 threads on 2 lines, profiles/r04/service_load_wpl.txt).
 bool service_gate_open(Service& sv) {
-    const int64_t m = pcs::get_tuning(kTuneServiceMaxCallers);
+    const int64_t m = std::min<int64_t>(pcs::get_tuning(kTuneServiceMaxCallers), 1 << 20);  // (m + 8) << 8 fits
     if (m <= 0) return true;
     const int limit = (int)((m + sv.lines - 1) << 8);
     const int a = sv.load.load(std::memory_order_relaxed);
@@ -756,7 +773,26 @@ void service_release(ServiceReq& r) {
 }
 
 std::atomic<uint64_t> g_torn_requests{0};
+std::atomic<uint64_t> g_reposts{0};  // PCS_COUNTER_SERVICE_REPOSTS
 thread_local int t_line_hint = -1;  // the line this thread used last: its first try
+
+// PCS_TUNE_SERVICE_REPOST_TEST (test only): post a request as an earlier
+// generation would have left it, partly answered, so the re-post path must
+// re-arm it.  seq names generation gen - 1, which no waiting kernel serves
+// (its kernel was queued before the current one and has left or leaves at
+// its next poll); the verdict words of pages 16 and up hold a stale answer
+// (validate: 0, a verdict no good page deserves; stamp: 1, a done word for a
+// header never written).  A host that re-posted without re-arming would
+// collect those as answers.  Needs gen >= 2 (generation gen - 1 then had a
+// kernel and its event); otherwise the request is posted normally and the
+// knob is not consumed.
+constexpr int kTuneServiceRepostTest = PCS_TUNE_SERVICE_REPOST_TEST;
+uint32_t repost_drill(pcs::ServiceLine* ln, uint64_t n, bool stamp, uint32_t gen) {
+    if (gen < 2 || pcs::get_tuning(kTuneServiceRepostTest) <= 0 || !pcs::take_tuning(kTuneServiceRepostTest))
+        return gen;
+    for (uint64_t i = 16; i < n; ++i) ln->ok[i] = stamp ? 1u : 0u;
+    return gen - 1;
+}
 
 // Claim a free line and post a validate (stamp = false) or stamp request:
 // XXH3, registered 16-byte-aligned pages with page_size % 256 == 0, 1..256
@@ -765,8 +801,7 @@ thread_local int t_line_hint = -1;  // the line this thread used last: its first
 // error.
 int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64_t P, uint64_t n, int algo,
                    bool stamp) {
-    if (!svp || algo != PCS_XXH3_64 || n == 0 || n > (uint64_t)pcs::kServiceMaxPages || !pcs::list_shape_ok(0, P))
-        return kNotServed;
+    if (!svp || !service_shape_ok(P, n, algo)) return kNotServed;
     Service& sv = *svp;
     if (!service_gate_open(sv)) return kNotServed;
     const int nl = std::max(1, std::min(sv.lines.load(std::memory_order_relaxed), pcs::kServiceMaxLines));
@@ -821,12 +856,13 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
         std::atomic_thread_fence(std::memory_order_release);
         __atomic_store_n(&ln->check, c, __ATOMIC_RELEASE);
         r.seq = seq;
+        r.gen = sv.gen.load(std::memory_order_relaxed);
     } else {
         ln->n = n;
         ln->page_size = page_word;
-        r.seq = service_post_locked(sv, k);
+        r.gen = repost_drill(ln, n, stamp, sv.gen.load(std::memory_order_relaxed));
+        r.seq = service_post_locked(sv, k, r.gen);
     }
-    r.gen = sv.gen.load(std::memory_order_relaxed);
     r.posted = r.checked = Service::clock::now();
     return PCS_OK;
 }
@@ -880,8 +916,17 @@ int service_progress(ServiceReq& r) {
             (void)service_reset_locked(sv);
             return rc;
         }
-    r.seq = service_post_locked(sv, r.k);
+    // Re-arm the whole request: verdicts the old generation left must not
+    // count as answers of the new one, whose workgroups re-hash those pages
+    // (and would otherwise still be doing so once the host had released the
+    // line).  No workgroup writes this line now: its kernel has left and the
+    // newer ones serve only the seq posted below.
+    uint32_t* ok = sv.h->line[r.k].ok;
+    for (uint64_t i = 0; i < r.n; ++i) ok[i] = pcs::kServicePending;
+    r.landed = 0;
+    g_reposts.fetch_add(1, std::memory_order_relaxed);
     r.gen = sv.gen.load(std::memory_order_relaxed);
+    r.seq = service_post_locked(sv, r.k, r.gen);
     r.posted = Service::clock::now();
     return 0;
 }
@@ -927,6 +972,7 @@ int service_run(Service* svp, const void* const* pages, uint64_t P, uint64_t n, 
 
 // Device copy of one host buffer + a result word, for the manifest host API.
 int manifest_host(const void* content, uint64_t len, uint64_t* out) {
+    if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
     if (int rc = require_device()) return rc;
     if (!out || (len && !content)) return fail(PCS_ERR_INVALID, "null pointer");
     int dev = 0;
@@ -1213,7 +1259,7 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
     if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
     if (g_services_on.load(std::memory_order_relaxed) > 0) {
         if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
-        CallerGuard g(current_service());
+        CallerGuard g(current_service(), page_size, n_pages, algo);
         const int r = service_run(g.service(), pages, page_size, n_pages, algo, ok, first_bad);
         if (r != kNotServed) return r;
         return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
@@ -1305,7 +1351,7 @@ int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_page
     if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
     if (g_services_on.load(std::memory_order_relaxed) > 0) {
         if (int rc = check_host_batch_args(cp, page_size, n_pages, algo)) return rc;
-        CallerGuard g(current_service());
+        CallerGuard g(current_service(), page_size, n_pages, algo);
         const int r = service_run(g.service(), cp, page_size, n_pages, algo, nullptr, nullptr);
         if (r != kNotServed) return r;
         return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);
@@ -1422,7 +1468,7 @@ int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64
     if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
     if (mode != PCS_BATCH_DIGEST && g_services_on.load(std::memory_order_relaxed) > 0) {
         Service* svp = current_service();
-        if (svp && svp->device >= 0) {
+        if (svp && svp->device >= 0 && service_shape_ok(P, n, algo)) {
             b->caller = svp;  // counted until the batch completes, on either path
             caller_enter(*svp);
             const int r = service_submit(b->svc, svp, pages, P, n, algo, mode == PCS_BATCH_STAMP);
@@ -1571,6 +1617,7 @@ int64_t pcs_get_tuning(int key) { return pcs::get_tuning(key); }
 
 uint64_t pcs_counter(int which) {
     if (which == PCS_COUNTER_SERVICE_TORN_REQUESTS) return g_torn_requests.load(std::memory_order_relaxed);
+    if (which == PCS_COUNTER_SERVICE_REPOSTS) return g_reposts.load(std::memory_order_relaxed);
     return (which < 0 || which > 3) ? 0 : g_counters[which].load(std::memory_order_relaxed);
 }
 

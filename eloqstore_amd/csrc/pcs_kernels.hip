@@ -1403,7 +1403,7 @@ uint64_t next_call_id() {
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 30;
+constexpr int kTuneKeys = 31;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1418,7 +1418,7 @@ constexpr int kTuneKeys = 30;
 // knob in commit 01e849b).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, true,  false, false, false, true};
+                                      false, true,  false, false, false, true,  false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1439,7 +1439,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*test only: validate service torn-line drill, microseconds*/ 0,
                                           /*test only: host-batch calls left to fail*/ 0,
                                           /*validate service contention gate: callers (0 = off)*/ 2,
-                                          /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0};
+                                          /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0,
+                                          /*test only: service requests left to post as a stale partial answer*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;

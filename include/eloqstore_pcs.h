@@ -88,8 +88,10 @@ enum pcs_flags {
  *      ignored, which pcs_abi_version() detects
  *   4  round 4: PCS_TUNE_SERVICE_TEAR_TEST / FAIL_INJECT / SERVICE_MAX_CALLERS,
  *      PCS_COUNTER_SERVICE_TORN_REQUESTS; the C++ single-page SetChecksum /
- *      ValidateChecksum moved to libeloqstore_pcs_dropin.so */
-#define PCS_ABI_VERSION 4
+ *      ValidateChecksum moved to libeloqstore_pcs_dropin.so
+ *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_COUNTER_SERVICE_REPOSTS
+ *      (additive: no prototype changed) */
+#define PCS_ABI_VERSION 5
 int pcs_abi_version(void);
 const char *pcs_version(void);
 const char *pcs_last_error(void);
@@ -303,7 +305,8 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     eligible calls on the device exceeds
  *                                     this + lines - 1 + 0.5, the service
  *                                     declines and calls take the launch
- *                                     path; 0 = off
+ *                                     path; 0 = off (values above 2^20 act
+ *                                     as 2^20: the gate never closes)
  *   PCS_TUNE_SERVICE_TEAR_TEST    [0] test only: microseconds the service's
  *                                     host side waits between posting seq and
  *                                     writing the request words (the kernel
@@ -313,6 +316,15 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     pcs_batch_poll / wait,
  *                                     pcs_manifest_*_host) fail with
  *                                     PCS_ERR_HIP; decremented per failure
+ *   PCS_TUNE_SERVICE_REPOST_TEST  [0] test only: the next k service requests
+ *                                     are posted as if an earlier generation
+ *                                     had answered part of them and left: seq
+ *                                     names the previous generation (no
+ *                                     waiting kernel serves it) and the
+ *                                     verdict words of pages 16 and up hold a
+ *                                     stale answer (validate 0, stamp 1); the
+ *                                     host must re-arm and re-post the whole
+ *                                     request (PCS_COUNTER_SERVICE_REPOSTS)
  * Keys 4, 5, 10, 12, 14, 16-22, 25 and 29 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -337,6 +349,7 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_TEAR_TEST = 26,
     PCS_TUNE_FAIL_INJECT = 27,
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
+    PCS_TUNE_SERVICE_REPOST_TEST = 30,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */
@@ -350,6 +363,8 @@ enum pcs_counter {
     PCS_COUNTER_SERVICE_BATCHES = 3,    /* validate / stamp batches served by the pre-armed service */
     PCS_COUNTER_SERVICE_TORN_REQUESTS = 4, /* served requests whose line the kernel first saw torn
                                               (new seq, words failing the check word) and ignored */
+    PCS_COUNTER_SERVICE_REPOSTS = 5,       /* service requests re-posted to a newer generation after
+                                              the kernel they were posted to left unanswered */
 };
 uint64_t pcs_counter(int which); /* 0 for an unknown counter */
 

@@ -193,6 +193,12 @@ static void abi4_no_device() {
     CHECK(pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS) == 0);
     CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_MAX_CALLERS) == 2 && pcs_get_tuning(29) == -1);
     CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && pcs_get_tuning(PCS_TUNE_SERVICE_TEAR_TEST) == 0);
+    // ABI 5: the re-post drill knob and counter
+    CHECK(PCS_ABI_VERSION >= 5 && pcs_get_tuning(PCS_TUNE_SERVICE_REPOST_TEST) == 0);
+    CHECK(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) == 0 && pcs_get_tuning(31) == -1);
+    // a huge gate knob is accepted (it acts as 2^20 callers: never closes)
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, INT64_MAX) == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
 
     std::vector<char> page(4096, 0x33);
     const char* cpages[1] = {page.data()};
@@ -208,6 +214,14 @@ static void abi4_no_device() {
     CHECK(std::strstr(eloqstore::LastChecksumError(), "injected failure") != nullptr);
     CHECK(eloqstore::TrySetChecksums(wpages, 4096) == PCS_ERR_HIP);
     CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && page[0] == 0x33);
+    // the manifest host calls consume injections too
+    CHECK(pcs_set_tuning(PCS_TUNE_FAIL_INJECT, 2) == PCS_OK);
+    uint64_t h = 0;
+    int valid = 7;
+    CHECK(pcs_manifest_checksum_host(page.data(), page.size(), &h) == PCS_ERR_HIP);
+    CHECK(pcs_manifest_validate_host(page.data(), page.size(), &valid) == PCS_ERR_HIP && valid == 7);
+    CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0);
+    CHECK(pcs_manifest_checksum_host(page.data(), page.size(), &h) == PCS_ERR_NO_DEVICE);
     // injections spent: the plain no-device failure again
     CHECK(eloqstore::TryValidateChecksums(cpages, 4096, ok, &fb) == PCS_ERR_NO_DEVICE);
     CHECK(std::strstr(eloqstore::LastChecksumError(), "no usable HIP device") != nullptr);

@@ -24,7 +24,9 @@
 // with a corrupted page, every stamp over a zeroed header) while a controller
 // thread keeps changing the service under them: stop, restart with 1-8 lines
 // of 1-4 workgroups and another idle time, gate knob 0/2/4, short torn-line
-// drills.  Every result must be exact on whichever path served it; prints
+// drills, and re-post drills (PCS_TUNE_SERVICE_REPOST_TEST: the next 1-4
+// requests are posted as a stale partial answer of an earlier generation,
+// which the host must re-arm and re-post).  Every result must be exact on whichever path served it; prints
 // the path mix, restarts and latency percentiles, then "service soak ok".
 #include <algorithm>
 #include <atomic>
@@ -133,6 +135,7 @@ int soak(char* pool, int T, double secs) {
     std::vector<std::vector<float>> lat(T);
     const Counts c0 = counts();
     const uint64_t torn0 = pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS);
+    const uint64_t reposts0 = pcs_counter(PCS_COUNTER_SERVICE_REPOSTS);
     CHECK(pcs_service_start_ex(2, 2, 0) == PCS_OK);
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -187,11 +190,11 @@ int soak(char* pool, int T, double secs) {
         });
     // the controller
     uint64_t rng = 0xC7A1ull;
-    int restarts = 0, gates = 0, drills = 0, stopped_ms = 0;
+    int restarts = 0, gates = 0, drills = 0, repost_drills = 0, stopped_ms = 0;
     const auto end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(secs));
     while (Clock::now() < end) {
         std::this_thread::sleep_for(std::chrono::microseconds(2000 + splitmix(rng) % 18000));
-        switch (splitmix(rng) % 4) {
+        switch (splitmix(rng) % 5) {
         case 0: {  // restart with another shape
             CHECK(pcs_service_stop() == PCS_OK);
             if (splitmix(rng) % 3 == 0) {  // a stretch with no service at all
@@ -212,17 +215,22 @@ int soak(char* pool, int T, double secs) {
             ++gates;
             break;
         }
-        default:  // a short torn-line drill under the running threads
+        case 3:  // a short torn-line drill under the running threads
             CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_TEAR_TEST, 20) == PCS_OK);
             std::this_thread::sleep_for(std::chrono::microseconds(500));
             CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_TEAR_TEST, 0) == PCS_OK);
             ++drills;
+            break;
+        default:  // the next few requests posted as stale partial answers: re-armed and re-posted
+            CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_REPOST_TEST, 1 + (int64_t)(splitmix(rng) % 4)) == PCS_OK);
+            ++repost_drills;
         }
     }
     done = true;
     for (auto& x : th) x.join();
     CHECK(pcs_service_stop() == PCS_OK);
     CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_REPOST_TEST, 0) == PCS_OK);
     const Counts c1 = counts();
     std::vector<float> all;
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
@@ -231,12 +239,13 @@ int soak(char* pool, int T, double secs) {
     const uint64_t total = n_sync + n_async + n_stamp;
     std::printf("soak %.0f s, %d threads: %llu requests exact (%llu sync validate, %llu async validate, %llu stamp; "
                 "%llu served, %llu launched), %d restarts (%d ms with no service), %d gate changes, %d torn drills "
-                "(%llu torn requests ignored)\n",
+                "(%llu torn requests ignored), %d re-post drills (%llu requests re-armed and re-posted)\n",
                 secs, T, (unsigned long long)total, (unsigned long long)n_sync.load(),
                 (unsigned long long)n_async.load(), (unsigned long long)n_stamp.load(),
                 (unsigned long long)(c1.served - c0.served), (unsigned long long)(c1.launched - c0.launched),
                 restarts, stopped_ms, gates, drills,
-                (unsigned long long)(pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS) - torn0));
+                (unsigned long long)(pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS) - torn0), repost_drills,
+                (unsigned long long)(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) - reposts0));
     std::printf("soak latency us: p50 %.1f  p99 %.1f  p99.9 %.1f  max %.1f\n", pct(0.5), pct(0.99), pct(0.999),
                 all.empty() ? 0.f : all.back());
     CHECK(c1.served > c0.served && c1.launched > c0.launched && restarts > 0);

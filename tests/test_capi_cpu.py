@@ -186,6 +186,8 @@ def test_counters_and_tuning_defaults():
     assert pcs.get_tuning(pcs.TUNE_SERVICE_TEAR_TEST) == 0
     assert pcs.get_tuning(pcs.TUNE_FAIL_INJECT) == 0
     assert pcs.lib().pcs_counter(pcs.COUNTER_SERVICE_TORN_REQUESTS) == 0
+    assert pcs.get_tuning(pcs.TUNE_SERVICE_REPOST_TEST) == 0
+    assert pcs.lib().pcs_counter(pcs.COUNTER_SERVICE_REPOSTS) == 0
 
 
 def test_skip_verify_flag_needs_no_gpu():

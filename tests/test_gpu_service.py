@@ -361,6 +361,139 @@ def test_service_native_threads_and_gate():
     print(r.stdout)
 
 
+def test_service_soak_under_restarts():
+    """tests/cpp/service_threads_test.cpp --soak: eight native threads mix
+    sync validates, async validates and stamps while a controller thread
+    stops and restarts the service with other line / workgroup / idle
+    shapes, flips the gate knob and runs torn-line and re-post drills under
+    them: every verdict, first_bad and header exact on whichever path served
+    it."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "service_threads_test")
+    r = subprocess.run([exe, "--soak", "12"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "service soak ok" in r.stdout, r.stdout + r.stderr
+    print(r.stdout)
+
+
+def two_generations(pool, P, idle_us=1000):
+    """Serve two requests an idle period apart, so the service has queued at
+    least two generations (the re-post drill needs generation gen - 1)."""
+    for _ in range(2):
+        ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(500, 504)), P)
+        assert ok.all() and fb is None
+        time.sleep(3 * idle_us / 1e6)
+
+
+@pytest.mark.parametrize("lines,wpl", [(1, 1), (2, 2), (4, 4)])
+def test_service_repost_rearms_stale_verdicts(lines, wpl):
+    """a request re-posted to a newer generation must be
+    re-armed, or verdicts an older generation left count as answers and a
+    lagging workgroup can write into the line's next request.  The drill
+    (PCS_TUNE_SERVICE_REPOST_TEST) posts each request as an earlier
+    generation would have left it: under generation gen - 1, which no
+    waiting kernel serves, with a stale answer in the verdict words of pages
+    16 and up (validate 0, stamp 1).  Every such request must come back
+    through one re-post (PCS_COUNTER_SERVICE_REPOSTS) with the oracle's
+    verdicts, first_bad and headers, and the next, undrilled request on the
+    same line must be exact too.  With one workgroup per line, page 16 is
+    hashed after page 0 by the same lanes, so a host that did not re-arm
+    would collect the stale 0 before it is overwritten."""
+    P = 4096
+    with stamped_pool(512, P, 0x5F8 + lines) as pool, pcs.ValidateService(wpl, 1000, lines):
+        two_generations(pool, P)
+        rng = np.random.default_rng(lines)
+        rep = pcs.COUNTER_SERVICE_REPOSTS
+        try:
+            for n, k in ((17, 3), (24, 20), (32, 0), (40, 16), (100, 99), (256, 7)):
+                idx = rng.permutation(256)[:n]
+                pool.pages[idx[k], 1234] ^= 0x08
+                r0, s0 = pcs.counter(rep), pcs.counter(SVC)
+                pcs.set_tuning(pcs.TUNE_SERVICE_REPOST_TEST, 1)
+                ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                assert pcs.get_tuning(pcs.TUNE_SERVICE_REPOST_TEST) == 0  # consumed by this request
+                want = np.ones(n, dtype=bool)
+                want[k] = False
+                assert fb == k and np.array_equal(ok.astype(bool), want), (n, k, fb, np.flatnonzero(~ok.astype(bool)))
+                assert pcs.counter(rep) == r0 + 1 and pcs.counter(SVC) == s0 + 1
+                pool.pages[idx[k], 1234] ^= 0x08
+                # the next request on the line (another page set): exact
+                other = 256 + rng.permutation(256)[:n]
+                ok, fb = pcs.validate_ptrs(pool.ptr(other), P)
+                assert ok.all() and fb is None and pcs.counter(rep) == r0 + 1
+            # stamps: a stale done word must not stand for a header never written
+            idx = np.arange(300, 340)
+            pool.pages[idx, :8] = 0
+            r0 = pcs.counter(rep)
+            pcs.set_tuning(pcs.TUNE_SERVICE_REPOST_TEST, 1)
+            pcs.stamp_ptrs(pool.ptr(idx), P)
+            want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0)
+            assert np.array_equal(pool.pages[idx, :8].copy().view(np.uint64).ravel(), want)
+            assert pcs.counter(rep) == r0 + 1
+            # and asynchronously
+            b = pcs.Batch()
+            try:
+                idx = np.arange(100, 160)
+                pool.pages[idx[30], 99] ^= 0x01
+                pcs.set_tuning(pcs.TUNE_SERVICE_REPOST_TEST, 1)
+                b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(idx), P)
+                b.wait()
+                ok, fb = b.result()
+                pool.pages[idx[30], 99] ^= 0x01
+                assert fb == 30 and sum(ok) == len(idx) - 1 and pcs.counter(rep) == r0 + 2
+            finally:
+                b.close()
+        finally:
+            pcs.set_tuning(pcs.TUNE_SERVICE_REPOST_TEST, 0)
+
+
+def test_service_restart_with_fewer_lines_falls_back():
+    """four async batches in flight, one on each line of a
+    4-line service, none answered (the re-post drill posts each under the
+    previous generation, with stale verdicts on pages 16 and up).  The
+    service stops and restarts with ONE line.  At their first check, the
+    three batches whose lines the new service does not serve re-run on the
+    launch path (pcs_capi.cpp: r.k >= lines, no re-post); the one on line 0
+    is re-armed and re-posted to the new service.  All four come back with
+    the oracle's verdicts and first_bad, and the restarted service serves
+    the next request."""
+    P = 4096
+    with stamped_pool(512, P, 0x5FA) as pool:
+        sets = [np.arange(40 * i, 40 * i + 20 + i) for i in range(4)]
+        bad = [3, 17, 5, 19]
+        batches = [pcs.Batch() for _ in range(4)]
+        rep = pcs.COUNTER_SERVICE_REPOSTS
+        try:
+            pcs._call("pcs_service_start_ex", 4, 2, 1000)
+            two_generations(pool, P)
+            for i, idx in enumerate(sets):
+                pool.pages[idx[bad[i]], 500] ^= 0x20
+            r0, (s0, z0) = pcs.counter(rep), counters()
+            pcs.set_tuning(pcs.TUNE_SERVICE_REPOST_TEST, 4)
+            for b, idx in zip(batches, sets):
+                b.submit_ptrs(pcs.Batch.VALIDATE, pool.ptr(idx), P)
+            assert pcs.get_tuning(pcs.TUNE_SERVICE_REPOST_TEST) == 0  # all four posted to the service
+            pcs._call("pcs_service_stop")
+            pcs._call("pcs_service_start_ex", 1, 2, 1000)
+            for i, b in enumerate(batches):
+                b.wait()
+                ok, fb = b.result()
+                assert fb == bad[i] and sum(ok) == len(sets[i]) - 1 and ok[bad[i]] == 0, (i, fb)
+            # one re-post (line 0) served by the new service; three launches
+            assert pcs.counter(rep) == r0 + 1
+            assert counters() == (s0 + 1, z0 + 3)
+            for i, idx in enumerate(sets):
+                pool.pages[idx[bad[i]], 500] ^= 0x20
+            s0, _ = counters()
+            ok, fb = pcs.validate_ptrs(pool.ptr(sets[2]), P)
+            assert ok.all() and fb is None and pcs.counter(SVC) == s0 + 1
+        finally:
+            pcs.set_tuning(pcs.TUNE_SERVICE_REPOST_TEST, 0)
+            for b in batches:
+                b.close()
+            pcs._call("pcs_service_stop")
+
+
 def test_service_async_batches(service):
     """ChecksumBatch (pcs_batch_*) validate and stamp batches posted to the
     service: submit returns at once, poll watches the verdict words;
