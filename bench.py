@@ -34,11 +34,17 @@ Also reported, on the same line:
                 pages and validating it like page_checksum_tool / page.cpp:25-31;
                 cpu_all_cores: the same over all usable host cores;
                 cpu_ref_inmem: the reference's xxhash.c over the same pages
-                already in memory, one thread (no pread per page); cpu_port:
+                already in memory, one thread (no pread per page);
+                cpu_ref_inmem_all_cores: the same on every usable core (the
+                node rate for host-resident pages); cpu_port:
                 the repo's C restatement likewise; cli_scan: this repo's GPU
                 CLI (--scan) over the same file.
   parity        sampled GPU digests (every 4096th page, first/last 64) against
-                the reference xxHash on the host.
+                the reference xxHash on the host, and the sampled page bodies
+                against the generator at their global page indices; with the
+                corruption drill, run on EVERY rank over its own shard
+                (parity_per_rank / drill_per_rank at N>1); the process exits
+                3 after printing the line if any rank fails either.
   sweep         (N=1) every other BASELINE config and mode, one entry each:
                 config 3 (XXH3 and XXH64), config 4, config 5, config 7 (16 KiB),
                 config 2 validate (read path) and stamp (write path), each with
@@ -267,8 +273,31 @@ def parity_sample(w: Workload, mode: str = "digest"):
     else:
         got = w.out.index_select(0, tidx).cpu().numpy().view(np.uint64)
     checker = "reference external/xxhash.c (oracle/_ref)" if oracle.ref_lib() is not None else "oracle C restatement"
-    return {"pages": int(len(idx)), "mismatches": int((want != got).sum()), "checker": checker,
-            "what": "headers written by the stamp" if mode == "stamp" else "GPU digests"}
+    res = {"pages": int(len(idx)), "mismatches": int((want != got).sum()), "checker": checker,
+           "what": "headers written by the stamp" if mode == "stamp" else "GPU digests"}
+    if w.P is not None:
+        # the sampled pages' bodies are the generator's pages at this rank's
+        # GLOBAL indices (first + i): the shard covers its own range
+        from workload import fill_pages_at
+        gen = fill_pages_at(w.seed, w.first + idx, w.P)
+        res["content_mismatches"] = int((gen[:, 8:] != host[:, 8:]).any(axis=1).sum())
+        res["global_pages"] = [int(w.first), int(w.first + w.n)]
+    return res
+
+
+def gather_checks(dist, world: int, rank: int, parity, drill):
+    """Every rank's parity sample and drill, gathered on every rank (gloo):
+    ([{"rank", "parity", "corruption_drill"}, ...] in rank order, all pass)."""
+    checks = [{"rank": rank, "parity": parity, "corruption_drill": drill}]
+    if dist is not None:
+        checks = [None] * world
+        dist.all_gather_object(checks, {"rank": rank, "parity": parity, "corruption_drill": drill})
+    return checks, all(parity_ok(c["parity"], c["corruption_drill"]) for c in checks)
+
+
+def parity_ok(par, drill) -> bool:
+    return bool(par and drill and par.get("mismatches") == 0 and par.get("content_mismatches", 0) == 0
+                and drill.get("pass"))
 
 
 def cpu_model() -> str:
@@ -283,6 +312,14 @@ def cpu_model() -> str:
 
 def usable_cores() -> int:
     return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
+def cpu_threads() -> int:
+    """One thread per core this process may actually use: the affinity
+    mask, capped by a cgroup CPU quota when one is set (a GPU box shows every
+    core of the host but grants a share of them)."""
+    quota = cgroup_cpu_quota()
+    return usable_cores() if quota is None else max(1, min(usable_cores(), int(quota)))
 
 
 def cgroup_cpu_quota():
@@ -376,8 +413,7 @@ def config1(target_s: float, all_cores_s: float | None, workdir: str | None = No
             # one thread per core this process may actually use: the affinity
             # mask, capped by a cgroup CPU quota when one is set (a GPU box
             # shows every core of the host but grants a share of them)
-            quota = cgroup_cpu_quota()
-            T = usable_cores() if quota is None else max(1, min(usable_cores(), int(quota)))
+            T = cpu_threads()
             done = [0] * T
             fails = [0] * T
             stop = time.perf_counter() + all_cores_s
@@ -433,10 +469,46 @@ def config1(target_s: float, all_cores_s: float | None, workdir: str | None = No
                            f"external/xxhash.c v0.8.3 XXH3_64bits over [8, 4096) of every page (gcc -O2, SSE2, "
                            f"oracle/_ref), one thread",
                  "pages_failed": int((got != want).sum())}
+        # The same in-memory pages on every usable core: the
+        # reference's ValidateChecksum loop over pages already in the page
+        # pool (async_io_manager.cpp:353-366 after ReadPages), one thread per
+        # core on disjoint page ranges.  This, not the pread-bound
+        # cpu_all_cores, is the node rate a host-resident GPU path competes
+        # with.
+        inmem_all = None
+        if all_cores_s:
+            T = cpu_threads()
+            done = [0] * T
+            fails = [0] * T
+            stop = time.perf_counter() + all_cores_s
+
+            def run_mem(i):
+                b0, e0 = i * n // T, (i + 1) * n // T
+                part, hdr = data[b0 * P:e0 * P], want[b0:e0]
+                while time.perf_counter() < stop:
+                    got = oracle.ref_pages_digest(part, P, 0)  # ctypes: the GIL is released in the call
+                    done[i] += (e0 - b0) * P
+                    fails[i] += int((got != hdr).sum())
+
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=run_mem, args=(i,)) for i in range(T)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            dt = time.perf_counter() - t0
+            inmem_all = {"value": round(sum(done) / dt / GIB, 2), "unit": "GiB/s", "cores": T, "kind": "reference",
+                         "usable_cores": usable_cores(), "cgroup_cpu_quota": cgroup_cpu_quota(), "cpu": cpu_model(),
+                         "pages_failed": sum(fails),
+                         "sample": f"config 1 file in memory (one 1 GiB buffer), {T} threads (one per usable core) "
+                                   f"on disjoint page ranges, each running the reference's external/xxhash.c "
+                                   f"XXH3_64bits over [8, 4096) of its pages and comparing the header, "
+                                   f"~{all_cores_s:.0f} s"}
         del data
         r = subprocess.run([pcs.TOOL_PATH, "--scan", path, str(P)], capture_output=True, text=True, timeout=300)
         scan = {"rc": r.returncode, "line": r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr.strip()}
-        return {"cpu_baseline": one, "cpu_all_cores": allc, "cpu_port": port, "cpu_ref_inmem": inmem, "cli_scan": scan}
+        return {"cpu_baseline": one, "cpu_all_cores": allc, "cpu_port": port, "cpu_ref_inmem": inmem,
+                "cpu_ref_inmem_all_cores": inmem_all, "cli_scan": scan}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -881,11 +953,15 @@ def main():
     if args.mode != "digest":  # leave self.out holding this batch's digests for the parity leg
         w.step("digest")
         torch.cuda.synchronize()
-    parity = parity_sample(w) if rank == 0 else None
+    # Parity and the corruption drill on EVERY rank, each over its own shard
+    # (SURVEY §8d "parity in every run", §8e partitioning); rank 0's line
+    # carries them all and the run fails if any rank's does.
+    parity = parity_sample(w)
     stream_rate = w.stream_read(max(3, args.steps // 20))
     time.sleep(PHASE_GAP_S)
-    drill = w.corruption_drill() if rank == 0 else None
+    drill = w.corruption_drill()
     time.sleep(PHASE_GAP_S)
+    per_rank_checks, checks_ok = gather_checks(dist, world, rank, parity, drill)
     # Optional legs, each guarded: a failure is recorded under its key and the
     # headline line (roofline, parity, drill) still prints.  The sweep runs
     # before config 1: with config 1 first (its CLI processes initialise the
@@ -904,7 +980,7 @@ def main():
     c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         all_s = None if args.no_all_cores else min(args.cpu_seconds, 5.0)
-        need = args.cpu_seconds + (all_s or 0) + 3.0 + 30.0  # + port leg + gen/scan/warm margin
+        need = args.cpu_seconds + 2 * (all_s or 0) + 3.0 + 30.0  # + port leg + gen/scan/warm margin
         if time.perf_counter() + need > deadline:
             c1 = {"skipped": f"bench wall budget: {deadline - time.perf_counter():.0f} s left, ~{need:.0f} s needed"}
         else:
@@ -966,8 +1042,12 @@ def main():
             "parity": parity,
         }
         line["corruption_drill"] = drill
+        if world > 1:
+            line["parity_per_rank"] = [dict(c["parity"], rank=c["rank"]) for c in per_rank_checks]
+            line["drill_per_rank"] = [dict(c["corruption_drill"], rank=c["rank"]) for c in per_rank_checks]
+        line["checks_all_ranks_pass"] = checks_ok
         if c1 is not None:
-            for k in ("cpu_all_cores", "cpu_port", "cpu_ref_inmem", "cli_scan"):
+            for k in ("cpu_all_cores", "cpu_port", "cpu_ref_inmem", "cpu_ref_inmem_all_cores", "cli_scan"):
                 line[k] = c1.get(k)
             for k in ("error", "skipped"):
                 if k in c1:
@@ -982,6 +1062,10 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if not checks_ok:
+        bad = [c["rank"] for c in per_rank_checks if not parity_ok(c["parity"], c["corruption_drill"])]
+        print(f"bench: parity or corruption drill failed on rank(s) {bad}", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

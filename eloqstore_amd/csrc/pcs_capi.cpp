@@ -172,7 +172,7 @@ int64_t zero_copy_policy() { return pcs::get_tuning(PCS_TUNE_ZERO_COPY); }
 // host wrote before the batch, its results are complete, and the host can
 // stop waiting without the stream's completion signal (PCS_TUNE_ZC_POLL = 1;
 // 5-6 us less per call).  The stream still orders the next
-// batch behind this one.  Zero-copy XXH3 stamps of up to kZcStampPollPages
+// batch behind this one.  Zero-copy XXH3 stamps of up to PCS_TUNE_ZC_STAMP_POLL_PAGES
 // wait the same way on a done byte per page, which the list kernel stores
 // after a system-scope release that follows the page's header.
 constexpr uint8_t kVerdictPending = 0xA5;
@@ -381,12 +381,13 @@ int check_host_batch_args(const void* const* pages, uint64_t P, uint64_t n, int 
     return PCS_OK;
 }
 
-// Zero-copy stamps of up to this many pages complete from per-page done
-// bytes (each released after its header) rather than the stream's signal:
-// 14.8 vs 19.6 us for one page, 22.2 vs 25.5 for 128; at 256 pages the
-// per-page release costs more than it saves (36.4 vs 33.4 us;
-// profiles/r03/crossover_stamp_poll.txt).
-constexpr uint64_t kZcStampPollPages = 128;
+// Zero-copy XXH3 stamps of up to PCS_TUNE_ZC_STAMP_POLL_PAGES pages complete
+// from per-page done bytes (each released after its header) rather than the
+// stream's signal (PCS_TUNE_ZC_POLL on).  The default comes from
+// integration_snippets --crossover with the columns in a fresh random order
+// every repetition (round 4's fixed-order columns had a 16 %
+// order bias).
+bool zc_stamp_poll(uint64_t n) { return n <= (uint64_t)pcs::get_tuning(PCS_TUNE_ZC_STAMP_POLL_PAGES); }
 
 // mode 0: digests -> out_dig;  mode 1: verdicts -> out_ok (+ first_bad);
 // mode 2: digests stamped into the caller's pages.
@@ -410,7 +411,7 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
         hipStream_t zs = ctx.slot[0].stream;
         // validate: completion from the landed verdicts; small XXH3 stamps:
         // from a done byte per page the kernel writes after each header
-        const bool poll_stamp = mode == 2 && algo == PCS_XXH3_64 && n <= kZcStampPollPages;
+        const bool poll_stamp = mode == 2 && algo == PCS_XXH3_64 && zc_stamp_poll(n);
         const bool poll = (mode == 1 || poll_stamp) && zc_poll();
         if (poll) arm_verdicts(ctx.zc.h_ok, n);
         e = pcs::run_list(mode, algo, ctx.zc.d_ptrs, ctx.zc.h_ptrs, P, n, mode == 0 ? ctx.zc.d_dig : nullptr,
@@ -1115,7 +1116,7 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
     // validate: completion from the landed verdicts; small zero-copy XXH3
     // stamps: from the per-page done bytes (each released after the header
     // and the digest word)
-    const bool poll_stamp = mode == PCS_BATCH_STAMP && b->zero_copy && algo == PCS_XXH3_64 && n <= kZcStampPollPages;
+    const bool poll_stamp = mode == PCS_BATCH_STAMP && b->zero_copy && algo == PCS_XXH3_64 && zc_stamp_poll(n);
     b->zc_polled = (mode == PCS_BATCH_VALIDATE || poll_stamp) && zc_poll();
     b->zc_landed = 0;
     if (b->zc_polled) arm_verdicts(b->zero_copy ? b->zc.h_ok : b->h_ok, n);

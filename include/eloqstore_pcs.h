@@ -89,8 +89,8 @@ enum pcs_flags {
  *   4  round 4: PCS_TUNE_SERVICE_TEAR_TEST / FAIL_INJECT / SERVICE_MAX_CALLERS,
  *      PCS_COUNTER_SERVICE_TORN_REQUESTS; the C++ single-page SetChecksum /
  *      ValidateChecksum moved to libeloqstore_pcs_dropin.so
- *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_COUNTER_SERVICE_REPOSTS
- *      (additive: no prototype changed) */
+ *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
+ *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed) */
 #define PCS_ABI_VERSION 5
 int pcs_abi_version(void);
 const char *pcs_version(void);
@@ -293,10 +293,15 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_ZC_POLL              [1] validate batches from host memory, sync
  *                                     and async, zero-copy AND staged (gather
  *                                     or direct DMA), plus zero-copy XXH3
- *                                     stamps of <= 128 pages: complete once
+ *                                     stamps of <= PCS_TUNE_ZC_STAMP_POLL_PAGES
+ *                                     pages: complete once
  *                                     every verdict / done byte has landed in
  *                                     host memory (1) or on the launch's
  *                                     completion signal (0)
+ *   PCS_TUNE_ZC_STAMP_POLL_PAGES [128] zero-copy XXH3 stamps of up to this
+ *                                     many pages complete from per-page done
+ *                                     bytes (with PCS_TUNE_ZC_POLL on), larger
+ *                                     ones on the launch's completion signal
  *   PCS_TUNE_SERVICE_STREAM       [1] stream of the validate service, read at
  *                                     pcs_service_start: 1 highest priority
  *                                     (hardware queues of its own), 0 plain
@@ -350,6 +355,7 @@ enum pcs_tune_key {
     PCS_TUNE_FAIL_INJECT = 27,
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
     PCS_TUNE_SERVICE_REPOST_TEST = 30,
+    PCS_TUNE_ZC_STAMP_POLL_PAGES = 31,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -47,3 +47,24 @@ def test_config1_failure_still_prints_the_line():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert "PCS_BENCH_FAIL_CONFIG1" in d["error"] and d["value"] is None
+
+
+def test_parity_ok_needs_every_check():
+    """A rank passes only with zero digest mismatches, zero content
+    mismatches (pages at its global indices) and a passing drill; bench.py
+    exits 3 after the line when any rank does not."""
+    good = {"mismatches": 0, "content_mismatches": 0}
+    assert bench.parity_ok(good, {"pass": True})
+    assert bench.parity_ok({"mismatches": 0}, {"pass": True})  # descriptor batches: no content check
+    assert not bench.parity_ok(dict(good, mismatches=1), {"pass": True})
+    assert not bench.parity_ok(dict(good, content_mismatches=2), {"pass": True})
+    assert not bench.parity_ok(good, {"pass": False})
+    assert not bench.parity_ok(None, {"pass": True}) and not bench.parity_ok(good, None)
+
+
+def test_fill_pages_at_matches_contiguous_generator():
+    from workload import fill_pages, fill_pages_at
+    import numpy as np
+    idx = np.array([5, 0, 4096, 77, 8191], dtype=np.int64)
+    whole = fill_pages(0x5EED0005, 0, 8192, 256)
+    assert np.array_equal(fill_pages_at(0x5EED0005, idx, 256), whole[idx])

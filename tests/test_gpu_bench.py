@@ -56,15 +56,19 @@ def test_config1_leg_on_the_real_file():
     reference's own xxHash validates every page on one thread, the repo's C
     restatement re-digests them, and the CLI's --scan scrubs the file: all
     must agree (tools/page_checksum_tool.cpp:94-105, page.cpp:25-31)."""
-    d = _one_line(subprocess.run([sys.executable, "bench.py", "--config", "1", "--cpu-seconds", "1",
-                                  "--no-all-cores"], cwd=ROOT, capture_output=True, text=True, timeout=300))
+    d = _one_line(subprocess.run([sys.executable, "bench.py", "--config", "1", "--cpu-seconds", "1"],
+                                 cwd=ROOT, capture_output=True, text=True, timeout=300))
     assert "error" not in d, d
     one = d["cpu_baseline"]
     assert one["kind"] == "reference" and one["cores"] == 1 and one["value"] > 0
     assert one["pages_failed"] == 0
     assert d["cpu_port"]["pages_failed"] == 0 and d["cpu_port"]["value"] > 0
+    assert d["cpu_ref_inmem"]["pages_failed"] == 0 and d["cpu_ref_inmem"]["cores"] == 1
     assert d["cli_scan"]["rc"] == 0, d["cli_scan"]
-    assert d["cpu_all_cores"] is None
+    # every usable core: pread loop and in-memory pages (VERDICT r04 #3)
+    for k in ("cpu_all_cores", "cpu_ref_inmem_all_cores"):
+        assert d[k]["pages_failed"] == 0 and d[k]["cores"] >= 1 and d[k]["value"] > 0, d[k]
+    assert d["cpu_ref_inmem_all_cores"]["cores"] == d["cpu_all_cores"]["cores"]
     assert not os.listdir(os.path.join(ROOT, ".bench_tmp")), "config-1 file left behind"
 
 

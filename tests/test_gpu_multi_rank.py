@@ -93,6 +93,14 @@ def test_bench_two_ranks_torchrun():
     assert line["config"]["pages_per_gpu"] == 1 << 23 and line["config"]["bytes_per_gpu"] == 32 << 30
     assert line["value"] > 0 and line["aggregate_roofline"]["peak_GBps"] == 2 * 8000.0
     assert line["corruption_drill"]["pass"] and line["parity"]["mismatches"] == 0
+    # parity and the drill on every rank, over its own shard
+    assert line["checks_all_ranks_pass"] is True
+    assert [p["rank"] for p in line["parity_per_rank"]] == [0, 1]
+    assert [d["rank"] for d in line["drill_per_rank"]] == [0, 1]
+    for p in line["parity_per_rank"]:
+        assert p["mismatches"] == 0 and p["content_mismatches"] == 0 and p["pages"] > 2000
+    assert [p["global_pages"] for p in line["parity_per_rank"]] == [[0, 1 << 23], [1 << 23, 2 << 23]]
+    assert all(d["pass"] and d["pages"] == 1 << 23 for d in line["drill_per_rank"])
     sd = line["scaling_detail"]
     assert [p["rank"] for p in sd["per_rank"]] == [0, 1]
     assert all(p["kernel_event_ms_per_step"] > 0 and p["wall_s"] > 0 for p in sd["per_rank"])

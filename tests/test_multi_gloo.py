@@ -49,10 +49,17 @@ def worker(rank: int, world: int, port: int, out_dir: str):
     bench.barrier(dist)
     mx = bench.max_over_ranks(dist, float(rank + 1))
     sm = bench.sum_over_ranks(dist, float(e - b))
+    # bench.py's per-rank parity gather: rank 1 reports a mismatch, so the
+    # gathered verdict must fail on every rank and name rank 1
+    par = {"pages": e - b, "mismatches": rank, "content_mismatches": 0}
+    checks, ok = bench.gather_checks(dist, world, rank, par, {"pass": True})
     if rank == 0:
         np.save(os.path.join(out_dir, "gathered.npy"), gathered.numpy())
         with open(os.path.join(out_dir, "stats.txt"), "w") as f:
             f.write(f"{mx} {sm}\n")
+        with open(os.path.join(out_dir, "checks.txt"), "w") as f:
+            bad = [c["rank"] for c in checks if not bench.parity_ok(c["parity"], c["corruption_drill"])]
+            f.write(f"{[c['rank'] for c in checks]} {ok} {bad}\n")
     dist.destroy_process_group()
 
 
@@ -67,3 +74,4 @@ def test_two_rank_shards_match_single_process(tmp_path):
     assert np.array_equal(gathered, single)
     mx, sm = open(tmp_path / "stats.txt").read().split()
     assert float(mx) == world and float(sm) == N_PAGES
+    assert open(tmp_path / "checks.txt").read().strip() == "[0, 1] False [1]"

@@ -42,6 +42,17 @@ def fill_pages(seed: int, first_page: int, n_pages: int, page_size: int) -> np.n
     return out.view(np.uint8).reshape(n_pages, page_size)
 
 
+def fill_pages_at(seed: int, page_indices, page_size: int) -> np.ndarray:
+    """(len(page_indices), page_size) uint8 array: the synthetic pages at
+    those global indices (any order, gaps allowed)."""
+    words = page_size // 8
+    with np.errstate(over="ignore"):
+        p = (np.asarray(page_indices, dtype=np.uint64) ^ np.uint64(seed))[:, None]
+        w = np.arange(1, words + 1, dtype=np.uint64)[None, :]
+        out = _mix(p + w * GOLDEN)
+    return out.view(np.uint8).reshape(len(page_indices), page_size)
+
+
 def mixed_sizes(seed: int, first_page: int, n: int) -> np.ndarray:
     with np.errstate(over="ignore"):
         p = np.arange(first_page, first_page + n, dtype=np.uint64) ^ np.uint64(seed)
