@@ -245,13 +245,21 @@ __device__ __forceinline__ void xxh3_list_body(PageAt page_at, uint32_t P, uint6
             h = xxh3_page_rt4<false>(page, P, L, stored);
         }
         if (L.g == 0) {
-            emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, nullptr);
             if (MODE == kStamp && ok) {
                 // small stamp batches: a done byte per page that the host
-                // polls instead of the completion signal, released after the
-                // header so it never lands first
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                st_nt(ok + pg, (uint8_t)1);
+                // polls instead of the completion signal.  The header and
+                // the done byte are system-scope stores, the byte released
+                // after the header, as the validate service writes them.
+                // With the header as a non-temporal store behind a release
+                // fence, the host saw the done byte before the header ~1 in
+                // 10^5 stamps under eight threads (service_threads_test
+                // --soak, profiles/r05/soak_bisect.txt).
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(page)), h, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                if (out) st_nt(out + pg, h);
+                __hip_atomic_store(ok + pg, (uint8_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, nullptr);
             }
         }
     }
