@@ -383,10 +383,12 @@ int check_host_batch_args(const void* const* pages, uint64_t P, uint64_t n, int 
 
 // Zero-copy XXH3 stamps of up to PCS_TUNE_ZC_STAMP_POLL_PAGES pages complete
 // from per-page done bytes (each released after its header) rather than the
-// stream's signal (PCS_TUNE_ZC_POLL on).  The default comes from
-// integration_snippets --crossover with the columns in a fresh random order
-// every repetition (round 4's fixed-order columns had a 16 %
-// order bias).
+// stream's signal (PCS_TUNE_ZC_POLL on).  The default (256, a full
+// FlushBatchPages batch) comes from integration_snippets --crossover with the
+// columns in a fresh random order every repetition: done bytes beat the
+// signal at every size to 256 (15.2 vs 20.3 us for one page, 33.5 vs 35.0 for
+// 256; profiles/r05/crossover_r05e.txt).  Round 4's fixed-order columns had
+// put the limit at 128 on a 16 % order bias.
 bool zc_stamp_poll(uint64_t n) { return n <= (uint64_t)pcs::get_tuning(PCS_TUNE_ZC_STAMP_POLL_PAGES); }
 
 // mode 0: digests -> out_dig;  mode 1: verdicts -> out_ok (+ first_bad);
@@ -1021,6 +1023,7 @@ struct pcs_batch {
     bool zero_copy = false;  // in-flight batch reads registered pages in place
     bool zc_polled = false;  // completion seen from the landed verdicts / done bytes (zc_poll)
     uint64_t zc_landed = 0;  // verdicts seen so far
+    uint32_t zc_polls = 0;   // polls since submit (the stream is queried every kZcEventQueryPolls-th)
     uint64_t n = 0, P = 0, first_bad = UINT64_MAX;
     int mode = 0, state = 0;  // 0 idle, 1 in flight, 2 done, -1 failed
     int algo = 0;
@@ -1119,6 +1122,7 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
     const bool poll_stamp = mode == PCS_BATCH_STAMP && b->zero_copy && algo == PCS_XXH3_64 && zc_stamp_poll(n);
     b->zc_polled = (mode == PCS_BATCH_VALIDATE || poll_stamp) && zc_poll();
     b->zc_landed = 0;
+    b->zc_polls = 0;
     if (b->zc_polled) arm_verdicts(b->zero_copy ? b->zc.h_ok : b->h_ok, n);
     if (b->zero_copy) {
         // stamp writes digests into the pages and into zc.h_dig (the digest
@@ -1145,6 +1149,8 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
     b->state = 1;
     return PCS_OK;
 }
+
+constexpr uint32_t kZcEventQueryPolls = 256;
 
 // Progress of a batch the service took: 1 done, 0 in flight (also after it
 // was moved to the launch path), < 0 failed.
@@ -1505,6 +1511,11 @@ int pcs_batch_poll(pcs_batch* b) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return batch_finalize(b);
         }
+        // Completion comes from the verdicts; the stream is asked only now
+        // and then, for a failed launch.  A query on every spin of a shard's
+        // poll loop cost a 192-256-page async validate 4.5 us against the
+        // synchronous call (profiles/r05/crossover_r05e.txt).
+        if (++b->zc_polls % kZcEventQueryPolls != 0) return 0;
     }
     const hipError_t e = hipEventQuery(b->done);
     if (e == hipErrorNotReady) return 0;

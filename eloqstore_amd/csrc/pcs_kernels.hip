@@ -1459,7 +1459,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*validate service contention gate: callers (0 = off)*/ 2,
                                           /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0,
                                           /*test only: service requests left to post as a stale partial answer*/ 0,
-                                          /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 128};
+                                          /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 256};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;

@@ -56,12 +56,14 @@ enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 // (types.h:31, scan_task.cpp:215), short overflow reads (task.cpp:136), the
 // tail of a write batch.  Defaults are the measured latency crossovers of one
 // call against one core running the reference loop over the same scattered
-// 4 KiB pool pages (integration_snippets --crossover):
-//   registered pool (RegisterPagePool, zero-copy): GPU faster from 32-48
-//   pages (two boxes; 40 pages = 160 KiB is the default);
-//   unregistered pages (gathered into staging):    GPU faster from 192 pages.
-inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(160) << 10;
-inline constexpr size_t kGpuChecksumMinBatchBytesStaged = size_t(768) << 10;
+// 4 KiB pool pages (integration_snippets --crossover, every repetition timing
+// the columns in a fresh random order, with a control column that must agree
+// within 3 %; DESIGN.md §5, profiles/r05/crossover_r05e.txt):
+//   registered pool (RegisterPagePool, zero-copy): GPU faster from 32 pages
+//   to validate and to stamp (32 pages = 128 KiB);
+//   unregistered pages (gathered into staging):    GPU faster from 256 pages.
+inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(128) << 10;
+inline constexpr size_t kGpuChecksumMinBatchBytesStaged = size_t(1) << 20;
 inline bool GpuChecksumPays(size_t n_pages, size_t page_size, size_t min_bytes = kGpuChecksumMinBatchBytes) {
     return n_pages * page_size >= min_bytes;
 }
@@ -113,9 +115,9 @@ void UnregisterPagePool(void* base);
 // batches of up to 256 registered pages are served through a resident kernel
 // polling a request line, instead of a launch per batch, and the GPU pays
 // from kGpuChecksumMinBatchBytesService on (4 KiB pool pages,
-// integration_snippets --crossover: one page 8.2-8.9 µs to validate instead
-// of 13.8-15.1 and 8.9 µs to stamp instead of 19.9; faster than the reference
-// loop from 20-24 pages to validate and 28-32 to stamp).  The kernel holds
+// integration_snippets --crossover, profiles/r05/crossover_r05e.txt: one page
+// 7.8 µs to validate instead of 14.8 and 8.2 µs to stamp instead of 15.2;
+// faster than the reference loop from 24 pages, both ways).  The kernel holds
 // `workgroups` CUs (16 serves 128-256 pages 10-15 % faster than 4) and
 // leaves after idle_us without a request or 2 * idle_us of life; the next
 // request starts a new one.  `lines` request lines (1-8) let that many calls
@@ -127,7 +129,7 @@ void UnregisterPagePool(void* base);
 // device has its own service.
 void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000, int lines = 1);
 void StopChecksumService();
-inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(128) << 10;
+inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(96) << 10;
 
 // Asynchronous batch for coroutine call sites: Submit, then Poll() from the
 // shard work loop (shard.cpp:67-130) until it returns true.  Pages must stay

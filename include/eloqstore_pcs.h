@@ -298,7 +298,7 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     every verdict / done byte has landed in
  *                                     host memory (1) or on the launch's
  *                                     completion signal (0)
- *   PCS_TUNE_ZC_STAMP_POLL_PAGES [128] zero-copy XXH3 stamps of up to this
+ *   PCS_TUNE_ZC_STAMP_POLL_PAGES [256] zero-copy XXH3 stamps of up to this
  *                                     many pages complete from per-page done
  *                                     bytes (with PCS_TUNE_ZC_POLL on), larger
  *                                     ones on the launch's completion signal

@@ -248,9 +248,10 @@ def test_zero_copy_validate_completion_forms(poll):
 @pytest.mark.parametrize("poll", [0, 1])
 @pytest.mark.parametrize("P", [4096, 8192, 1280])
 def test_zero_copy_stamp_completion_forms(poll, P):
-    """PCS_TUNE_ZC_POLL on stamps: a zero-copy XXH3 stamp of up to 128 pages
-    completes from per-page done bytes, each released after its header and
-    digest word (1), or on the completion signal (0).  Back-to-back sync
+    """PCS_TUNE_ZC_POLL on stamps: a zero-copy XXH3 stamp of up to
+    PCS_TUNE_ZC_STAMP_POLL_PAGES (256) pages completes from per-page done
+    bytes, each a system-scope store released after its header (1), or on the
+    completion signal (0).  Back-to-back sync
     stamps and async batches (poll and wait) with the pool's bytes rewritten
     between calls: every header (and an async batch's digests) must be the
     oracle's digest of the new bytes once the call returns, and pages outside
@@ -263,7 +264,7 @@ def test_zero_copy_stamp_completion_forms(poll, P):
             b = pcs.Batch()
             try:
                 for it in range(36):
-                    n = (1, 6, 48, 128, 129, 300)[it % 6]
+                    n = (1, 6, 48, 129, 256, 300)[it % 6]
                     form = it // 6 % 3  # sync call, async poll(), async wait()
                     pool.pages[:] = oracle.fill_pages(P, 512, 0x57A0 + it).reshape(512, P)
                     pool.pages[:, :8] = 0
