@@ -1129,7 +1129,12 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
         // result of a stamp batch)
         e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
                           mode == PCS_BATCH_VALIDATE || b->zc_polled ? b->zc.d_ok : nullptr, s);
-        if (e == hipSuccess) e = hipEventRecord(b->done, s);
+        // A batch that completes from its verdicts / done bytes needs no
+        // event behind the kernel (poll asks the stream itself, now and
+        // then): experiment on the 192-256-page async rows, which ran 4 us
+        // behind the synchronous call with the record in place
+        // (profiles/r05/crossover_r05f.txt).
+        if (e == hipSuccess && !b->zc_polled) e = hipEventRecord(b->done, s);
         if (e != hipSuccess) return hip_fail(e, "pcs_batch_submit (zero-copy)");
         count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
         b->state = 1;
@@ -1511,13 +1516,12 @@ int pcs_batch_poll(pcs_batch* b) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return batch_finalize(b);
         }
-        // Completion comes from the verdicts; the stream is asked only now
-        // and then, for a failed launch.  A query on every spin of a shard's
-        // poll loop cost a 192-256-page async validate 4.5 us against the
-        // synchronous call (profiles/r05/crossover_r05e.txt).
+        // Completion comes from the verdicts; the stream is asked only every
+        // kZcEventQueryPolls-th poll, for a launch that failed (the runtime
+        // call costs more than a scan of the verdict bytes).
         if (++b->zc_polls % kZcEventQueryPolls != 0) return 0;
     }
-    const hipError_t e = hipEventQuery(b->done);
+    const hipError_t e = b->zc_polled && b->zero_copy ? hipStreamQuery(b->stream) : hipEventQuery(b->done);
     if (e == hipErrorNotReady) return 0;
     if (e != hipSuccess) return batch_failed(b, hip_fail(e, "pcs_batch_poll"));
     return batch_finalize(b);
