@@ -1129,12 +1129,7 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
         // result of a stamp batch)
         e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
                           mode == PCS_BATCH_VALIDATE || b->zc_polled ? b->zc.d_ok : nullptr, s);
-        // A batch that completes from its verdicts / done bytes needs no
-        // event behind the kernel (poll asks the stream itself, now and
-        // then): experiment on the 192-256-page async rows, which ran 4 us
-        // behind the synchronous call with the record in place
-        // (profiles/r05/crossover_r05f.txt).
-        if (e == hipSuccess && !b->zc_polled) e = hipEventRecord(b->done, s);
+        if (e == hipSuccess) e = hipEventRecord(b->done, s);
         if (e != hipSuccess) return hip_fail(e, "pcs_batch_submit (zero-copy)");
         count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
         b->state = 1;
@@ -1521,7 +1516,7 @@ int pcs_batch_poll(pcs_batch* b) {
         // call costs more than a scan of the verdict bytes).
         if (++b->zc_polls % kZcEventQueryPolls != 0) return 0;
     }
-    const hipError_t e = b->zc_polled && b->zero_copy ? hipStreamQuery(b->stream) : hipEventQuery(b->done);
+    const hipError_t e = hipEventQuery(b->done);
     if (e == hipErrorNotReady) return 0;
     if (e != hipSuccess) return batch_failed(b, hip_fail(e, "pcs_batch_poll"));
     return batch_finalize(b);

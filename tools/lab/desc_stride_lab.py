@@ -9,7 +9,10 @@ The same 1 M descriptors, same sizes in the same order, placed
   shuffled   16 KiB slots in a random order (the page order no longer follows
              the address order)
 and, for the size mix alone, uniform pages packed (4, 8 and 16 KiB, the same
-kernel).  Each layout: 5 rounds x 20 launches bracketed by HIP events, the
+kernel).  Then the channel question: at a 16 KiB stride every group of a
+wave reads the same 4 KiB sub-block offset of its page at the same step
+(address bits 12-13 equal across the wave); at a 20 KiB stride (stride20k,
+uniform16k_s20k) the page starts rotate through those bits.  Each layout: 5 rounds x 20 launches bracketed by HIP events, the
 layouts interleaved round by round (A B C ... A B C ...), median round.
 frac = (sum of page bytes + 8 B digest per page) / time / 8 TB/s.
 
@@ -45,7 +48,7 @@ perm = np.random.default_rng(5).permutation(n).astype(np.uint64)
 shuffled = perm * np.uint64(16384)
 
 layouts = {}
-arena_bytes = n * 16384
+arena_bytes = n * 20480
 arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
 
 
@@ -58,9 +61,12 @@ def add(name, offs, ls):
 add("packed", packed, lens)
 add("stride16k", stride, lens)
 add("shuffled", shuffled, lens)
+add("stride20k", np.arange(n, dtype=np.uint64) * np.uint64(20480), lens)
 for P in (4096, 8192, 16384):
     ls = np.full(n, P, dtype=np.uint32)
     add(f"uniform{P // 1024}k", np.arange(n, dtype=np.uint64) * np.uint64(P), ls)
+add("uniform16k_s20k", np.arange(n, dtype=np.uint64) * np.uint64(20480), np.full(n, 16384, dtype=np.uint32))
+add("uniform8k_s12k", np.arange(n, dtype=np.uint64) * np.uint64(12288), np.full(n, 8192, dtype=np.uint32))
 pcs.gen_pages(arena, 4096, arena_bytes // 4096, seed, 0)  # bytes only: every layout reads the same arena
 out = torch.empty(n, dtype=torch.int64, device=dev)
 torch.cuda.synchronize()
