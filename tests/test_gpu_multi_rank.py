@@ -106,3 +106,22 @@ def test_bench_two_ranks_torchrun():
     assert all(p["kernel_event_ms_per_step"] > 0 and p["wall_s"] > 0 for p in sd["per_rank"])
     assert sd["concurrent_over_solo"] > 0 and sd["solo_rank0_GiBps"] > 0 and sd["shared_gpus"]
     assert "sweep" not in line  # the sweep is an N=1 leg
+
+
+def test_bench_four_ranks_torchrun():
+    """Four ranks on the box's one GPU (1 M pages per rank, config 5's seed and
+    global page indices): every rank's parity and drill come back in rank 0's
+    line, each over its own global range."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           "bench.py", "--gpus", "4", "--steps", "3", "--warmup", "1", "--pages-per-gpu", str(1 << 20)]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 4 and line["checks_all_ranks_pass"] is True
+    n = 1 << 20
+    assert [p["global_pages"] for p in line["parity_per_rank"]] == [[r * n, (r + 1) * n] for r in range(4)]
+    assert all(p["mismatches"] == 0 and p["content_mismatches"] == 0 for p in line["parity_per_rank"])
+    assert [d["rank"] for d in line["drill_per_rank"]] == [0, 1, 2, 3] and all(d["pass"] for d in line["drill_per_rank"])

@@ -513,6 +513,51 @@ def test_service_restart_with_fewer_lines_falls_back():
             pcs._call("pcs_service_stop")
 
 
+def test_gate_counts_only_service_shaped_calls():
+    """the contention gate counts only calls the service could
+    take (XXH3, 1-256 pages, page size on the 256-byte grid).  Four threads
+    hammering XXH64 validates (always the launch path) beside one thread of
+    small XXH3 validates on a one-line service with the gate at its default:
+    the XXH64 traffic must not close the gate, so the XXH3 thread stays
+    served (round 4 counted every call and closed it)."""
+    P = 4096
+    assert pcs.get_tuning(pcs.TUNE_SERVICE_MAX_CALLERS) == 2
+    with stamped_pool(512, P, 0x5FB) as pool, pcs.ValidateService(4, 1000, 1):
+        x64 = np.arange(256, 320)
+        pcs.stamp_ptrs(pool.ptr(x64), P, pcs.XXH64)
+        stop = threading.Event()
+        errors = []
+
+        def hammer():
+            try:
+                while not stop.is_set():
+                    ok, fb = pcs.validate_ptrs(pool.ptr(x64), P, pcs.XXH64)
+                    if not ok.all():
+                        errors.append("xxh64 verdicts")
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=hammer) for _ in range(4)]
+        for x in th:
+            x.start()
+        try:
+            time.sleep(0.05)
+            s0 = pcs.counter(SVC)
+            calls = 0
+            t_end = time.perf_counter() + 0.5
+            while time.perf_counter() < t_end:
+                ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(6)), P)
+                assert ok.all() and fb is None
+                calls += 1
+            served = pcs.counter(SVC) - s0
+        finally:
+            stop.set()
+            for x in th:
+                x.join()
+        assert not errors, errors[:3]
+        assert calls > 50 and served >= 0.9 * calls, (served, calls)
+
+
 def test_service_async_batches(service):
     """ChecksumBatch (pcs_batch_*) validate and stamp batches posted to the
     service: submit returns at once, poll watches the verdict words;

@@ -11,6 +11,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -51,7 +52,7 @@ def worker(rank: int, world: int, port: int, out_dir: str):
     sm = bench.sum_over_ranks(dist, float(e - b))
     # bench.py's per-rank parity gather: rank 1 reports a mismatch, so the
     # gathered verdict must fail on every rank and name rank 1
-    par = {"pages": e - b, "mismatches": rank, "content_mismatches": 0}
+    par = {"pages": e - b, "mismatches": int(rank == 1), "content_mismatches": 0}
     checks, ok = bench.gather_checks(dist, world, rank, par, {"pass": True})
     if rank == 0:
         np.save(os.path.join(out_dir, "gathered.npy"), gathered.numpy())
@@ -63,8 +64,8 @@ def worker(rank: int, world: int, port: int, out_dir: str):
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_match_single_process(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_shards_match_single_process(tmp_path, world):
     mp.spawn(worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
     import oracle
     from workload import fill_pages
@@ -74,4 +75,4 @@ def test_two_rank_shards_match_single_process(tmp_path):
     assert np.array_equal(gathered, single)
     mx, sm = open(tmp_path / "stats.txt").read().split()
     assert float(mx) == world and float(sm) == N_PAGES
-    assert open(tmp_path / "checks.txt").read().strip() == "[0, 1] False [1]"
+    assert open(tmp_path / "checks.txt").read().strip() == f"{list(range(world))} False [1]"
