@@ -1421,7 +1421,7 @@ bool is_pow2_page(uint64_t P) { return P >= 256 && P <= 65536 && (P & (P - 1)) =
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 32;
+constexpr int kTuneKeys = 33;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1436,7 +1436,7 @@ constexpr int kTuneKeys = 32;
 // knob in commit 01e849b).  Setting one fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, true,  false, false, false, true,  false, false};
+                                      false, true,  false, false, false, true,  false, false, false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1459,7 +1459,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*validate service contention gate: callers (0 = off)*/ 2,
                                           /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0,
                                           /*test only: service requests left to post as a stale partial answer*/ 0,
-                                          /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 256};
+                                          /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 256,
+                                          /*validate service: polls of the request line in flight (1, 2, 4)*/ 1};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1886,6 +1887,11 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // reaches host memory without a release fence.  A stamp request (high half
 // of the page-size word) stores the digest into the page header instead and
 // then a done word, released after it.
+// DEPTH polls of the line are kept in flight (round 5): each polling lane
+// issues its next load before it examines the previous one's result, so a
+// request that lands is seen after one PCIe read latency plus at most
+// 1 / DEPTH of one, instead of up to two (PCS_TUNE_SERVICE_POLL_DEPTH).
+template <int DEPTH>
 __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint64_t gen, uint64_t idle_ticks,
                                                  uint64_t life_ticks) {
     constexpr int W = kServiceLineWords;
@@ -1903,8 +1909,14 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
             const uint64_t* src = threadIdx.x < W ? &line->seq + threadIdx.x : &box->stop + (threadIdx.x - W);
             uint64_t w = 0;
             int go = 0;
+            uint64_t q[DEPTH];  // polls in flight, oldest first
+#pragma unroll
+            for (int i = 0; i + 1 < DEPTH; ++i) q[i] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             for (;;) {
-                w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                q[DEPTH - 1] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                w = q[0];  // the oldest poll: examined while the newer ones are in flight
+#pragma unroll
+                for (int i = 0; i + 1 < DEPTH; ++i) q[i] = q[i + 1];
                 const uint64_t w0 = __shfl(w, 0, 32);
                 // stop, or a newer generation queued behind this kernel
                 if (__shfl(w, W, 32) != 0 || __shfl(w, W + 1, 32) != gen) break;
@@ -1965,8 +1977,13 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
 hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                        hipStream_t s) {
     if (lines < 1 || lines > kServiceMaxLines || wpl < 1 || lines * wpl > 256) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_service, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, (uint64_t)gen,
-                       idle_ticks, life_ticks);
+    const int64_t depth = g_tune[32].load(std::memory_order_relaxed);
+#define L(D) hipLaunchKernelGGL(k_service<D>, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, \
+                                (uint64_t)gen, idle_ticks, life_ticks)
+    if (depth >= 4) L(4);
+    else if (depth == 2 || depth == 3) L(2);
+    else L(1);
+#undef L
     return hipGetLastError();
 }
 

@@ -90,7 +90,8 @@ enum pcs_flags {
  *      PCS_COUNTER_SERVICE_TORN_REQUESTS; the C++ single-page SetChecksum /
  *      ValidateChecksum moved to libeloqstore_pcs_dropin.so
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
- *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed) */
+ *      PCS_TUNE_SERVICE_POLL_DEPTH, PCS_COUNTER_SERVICE_REPOSTS (additive:
+ *      no prototype changed) */
 #define PCS_ABI_VERSION 5
 int pcs_abi_version(void);
 const char *pcs_version(void);
@@ -305,6 +306,10 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_SERVICE_STREAM       [1] stream of the validate service, read at
  *                                     pcs_service_start: 1 highest priority
  *                                     (hardware queues of its own), 0 plain
+ *   PCS_TUNE_SERVICE_POLL_DEPTH   [1] validate service: polls of the request
+ *                                     line each polling lane keeps in flight
+ *                                     (1, 2 or 4; read when a service kernel
+ *                                     is queued)
  *   PCS_TUNE_SERVICE_MAX_CALLERS  [2] validate service contention gate: while
  *                                     the decaying average of concurrent
  *                                     eligible calls on the device exceeds
@@ -356,6 +361,7 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
     PCS_TUNE_SERVICE_REPOST_TEST = 30,
     PCS_TUNE_ZC_STAMP_POLL_PAGES = 31,
+    PCS_TUNE_SERVICE_POLL_DEPTH = 32,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -195,7 +195,8 @@ static void abi4_no_device() {
     CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && pcs_get_tuning(PCS_TUNE_SERVICE_TEAR_TEST) == 0);
     // ABI 5: the re-post drill knob and counter
     CHECK(PCS_ABI_VERSION >= 5 && pcs_get_tuning(PCS_TUNE_SERVICE_REPOST_TEST) == 0);
-    CHECK(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) == 0 && pcs_get_tuning(32) == -1);
+    CHECK(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) == 0 && pcs_get_tuning(33) == -1);
+    CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_POLL_DEPTH) == 1);
     CHECK(pcs_get_tuning(PCS_TUNE_ZC_STAMP_POLL_PAGES) == 256);
     // a huge gate knob is accepted (it acts as 2^20 callers: never closes)
     CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, INT64_MAX) == PCS_OK);
