@@ -164,7 +164,6 @@ TUNE_FAIL_INJECT = 27  # test only
 TUNE_SERVICE_MAX_CALLERS = 28
 TUNE_SERVICE_REPOST_TEST = 30  # test only
 TUNE_ZC_STAMP_POLL_PAGES = 31
-TUNE_SERVICE_POLL_DEPTH = 32
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1

@@ -1433,10 +1433,12 @@ constexpr int kTuneKeys = 33;
 // descriptor body at 4 waves per SIMD (-0.6..-2.3 %, desc_lean_lab.txt);
 // round 3: 22 the XXH64 direct-to-LDS segment ring (config 3 -0.8..-34 %,
 // profiles/r03/x64_glds_ab_*.txt), 25 XXH64 tile-order chunks (no gain, a lab
-// knob in commit 01e849b).  Setting one fails.
+// knob in commit 01e849b); round 5: 32 service polls kept in flight (+0.7 to
+// +2.8 us per request, profiles/r05/service_poll_lab_r05k.txt).  Setting one
+// fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, true,  false, false, false, true,  false, false, false};
+                                      false, true,  false, false, false, true,  false, false, true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1460,7 +1462,7 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0,
                                           /*test only: service requests left to post as a stale partial answer*/ 0,
                                           /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 256,
-                                          /*validate service: polls of the request line in flight (1, 2, 4)*/ 1};
+                                          /*retired (round 5 lab: service polls in flight)*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1887,11 +1889,11 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // reaches host memory without a release fence.  A stamp request (high half
 // of the page-size word) stores the digest into the page header instead and
 // then a done word, released after it.
-// DEPTH polls of the line are kept in flight (round 5): each polling lane
-// issues its next load before it examines the previous one's result, so a
-// request that lands is seen after one PCIe read latency plus at most
-// 1 / DEPTH of one, instead of up to two (PCS_TUNE_SERVICE_POLL_DEPTH).
-template <int DEPTH>
+// One poll of the line in flight per lane.  Keeping 2 or 4 in flight (each
+// lane issuing its next load before examining the previous one) measured
+// +0.7 / +2.8 us per request (round 5, profiles/r05/service_poll_lab_r05k.txt):
+// the acquire that follows a served poll waits for the newer polls still in
+// flight, one more PCIe round trip on every request.
 __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint64_t gen, uint64_t idle_ticks,
                                                  uint64_t life_ticks) {
     constexpr int W = kServiceLineWords;
@@ -1909,14 +1911,8 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
             const uint64_t* src = threadIdx.x < W ? &line->seq + threadIdx.x : &box->stop + (threadIdx.x - W);
             uint64_t w = 0;
             int go = 0;
-            uint64_t q[DEPTH];  // polls in flight, oldest first
-#pragma unroll
-            for (int i = 0; i + 1 < DEPTH; ++i) q[i] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             for (;;) {
-                q[DEPTH - 1] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                w = q[0];  // the oldest poll: examined while the newer ones are in flight
-#pragma unroll
-                for (int i = 0; i + 1 < DEPTH; ++i) q[i] = q[i + 1];
+                w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 const uint64_t w0 = __shfl(w, 0, 32);
                 // stop, or a newer generation queued behind this kernel
                 if (__shfl(w, W, 32) != 0 || __shfl(w, W + 1, 32) != gen) break;
@@ -1977,13 +1973,8 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
 hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                        hipStream_t s) {
     if (lines < 1 || lines > kServiceMaxLines || wpl < 1 || lines * wpl > 256) return hipErrorInvalidValue;
-    const int64_t depth = g_tune[32].load(std::memory_order_relaxed);
-#define L(D) hipLaunchKernelGGL(k_service<D>, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, \
-                                (uint64_t)gen, idle_ticks, life_ticks)
-    if (depth >= 4) L(4);
-    else if (depth == 2 || depth == 3) L(2);
-    else L(1);
-#undef L
+    hipLaunchKernelGGL(k_service, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, (uint64_t)gen,
+                       idle_ticks, life_ticks);
     return hipGetLastError();
 }
 

@@ -90,8 +90,7 @@ enum pcs_flags {
  *      PCS_COUNTER_SERVICE_TORN_REQUESTS; the C++ single-page SetChecksum /
  *      ValidateChecksum moved to libeloqstore_pcs_dropin.so
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
- *      PCS_TUNE_SERVICE_POLL_DEPTH, PCS_COUNTER_SERVICE_REPOSTS (additive:
- *      no prototype changed) */
+ *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed) */
 #define PCS_ABI_VERSION 5
 int pcs_abi_version(void);
 const char *pcs_version(void);
@@ -306,10 +305,6 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *   PCS_TUNE_SERVICE_STREAM       [1] stream of the validate service, read at
  *                                     pcs_service_start: 1 highest priority
  *                                     (hardware queues of its own), 0 plain
- *   PCS_TUNE_SERVICE_POLL_DEPTH   [1] validate service: polls of the request
- *                                     line each polling lane keeps in flight
- *                                     (1, 2 or 4; read when a service kernel
- *                                     is queued)
  *   PCS_TUNE_SERVICE_MAX_CALLERS  [2] validate service contention gate: while
  *                                     the decaying average of concurrent
  *                                     eligible calls on the device exceeds
@@ -335,12 +330,13 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     stale answer (validate 0, stamp 1); the
  *                                     host must re-arm and re-post the whole
  *                                     request (PCS_COUNTER_SERVICE_REPOSTS)
- * Keys 4, 5, 10, 12, 14, 16-22, 25 and 29 selected variants that measured slower or no
+ * Keys 4, 5, 10, 12, 14, 16-22, 25, 29 and 32 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
  * tiles, plain result stores, 4 KiB-aligned descriptor steps, a 4-waves-
  * per-SIMD descriptor body; round 3: an XXH64 direct-to-LDS segment ring,
- * XXH64 tile-order chunks; round 4: XXH64 equal-byte runs per quad);
+ * XXH64 tile-order chunks; round 4: XXH64 equal-byte runs per quad; round 5:
+ * validate-service polls kept in flight);
  * they were retired: setting one fails and reading one
  * returns -1. */
 enum pcs_tune_key {
@@ -361,7 +357,6 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
     PCS_TUNE_SERVICE_REPOST_TEST = 30,
     PCS_TUNE_ZC_STAMP_POLL_PAGES = 31,
-    PCS_TUNE_SERVICE_POLL_DEPTH = 32,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

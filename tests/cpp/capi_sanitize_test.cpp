@@ -196,7 +196,7 @@ static void abi4_no_device() {
     // ABI 5: the re-post drill knob and counter
     CHECK(PCS_ABI_VERSION >= 5 && pcs_get_tuning(PCS_TUNE_SERVICE_REPOST_TEST) == 0);
     CHECK(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) == 0 && pcs_get_tuning(33) == -1);
-    CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_POLL_DEPTH) == 1);
+    CHECK(pcs_get_tuning(32) == -1 && pcs_set_tuning(32, 2) == PCS_ERR_INVALID);  // retired (round 5)
     CHECK(pcs_get_tuning(PCS_TUNE_ZC_STAMP_POLL_PAGES) == 256);
     // a huge gate knob is accepted (it acts as 2^20 callers: never closes)
     CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, INT64_MAX) == PCS_OK);

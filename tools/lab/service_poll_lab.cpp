@@ -1,11 +1,15 @@
 // service_poll_lab.cpp — validate-service latency against the number of
 // request-line polls each polling lane keeps in flight
-// (PCS_TUNE_SERVICE_POLL_DEPTH 1 / 2 / 4).  Not part of the product.  One
+// (32 /* PCS_TUNE_SERVICE_POLL_DEPTH, retired */ 1 / 2 / 4).  Not part of the product.  One
 // thread, a registered 1 GiB pool of 4 KiB pages, random pages per call.
 // The depth is read when a service kernel is queued, so each round sets it,
 // restarts the service (4 workgroups, one line, 1 ms idle), warms 50 calls
 // and times 300 calls per page count (page counts shuffled per repetition);
 // rounds cycle the depths (1 2 4 1 2 4 ...), medians over all rounds.
+//
+// Result (profiles/r05/service_poll_lab_r05k.txt): depth 1 fastest; the knob
+// (key 32) and the templated kernel were retired after this run, so this
+// lab now builds against raw key 32, which the library refuses.
 //
 //   make -C tools/lab $PWD/tools/lab/service_poll_lab && ./tools/lab/service_poll_lab [rounds]
 #include "eloqstore_pcs.h"
@@ -45,7 +49,7 @@ int main(int argc, char** argv) {
     CHECK(pcs_batch_create(&b) == PCS_OK);
     for (int r = 0; r < rounds * 3; ++r) {
         const int depth = depths[r % 3];
-        CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_POLL_DEPTH, depth) == PCS_OK);
+        CHECK(pcs_set_tuning(32 /* PCS_TUNE_SERVICE_POLL_DEPTH, retired */, depth) == PCS_OK);
         CHECK(pcs_service_start_ex(1, 4, 1000) == PCS_OK);
         const uint64_t served0 = pcs_counter(PCS_COUNTER_SERVICE_BATCHES);
         uint64_t calls = 0;
@@ -91,7 +95,7 @@ int main(int argc, char** argv) {
             std::printf("%5d  %5zu  %8.2f  %8.2f  %9.2f\n", d, n, med(sync_us[{d, n}]), pct(sync_us[{d, n}], 0.99),
                         med(async_us[{d, n}]));
     pcs_batch_destroy(b);
-    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_POLL_DEPTH, 1) == PCS_OK);
+    CHECK(pcs_set_tuning(32 /* PCS_TUNE_SERVICE_POLL_DEPTH, retired */, 1) == PCS_OK);
     CHECK(pcs_host_unregister(pool) == PCS_OK);
     std::free(pool);
     return 0;
