@@ -256,7 +256,9 @@ __device__ __forceinline__ void xxh3_list_body(PageAt page_at, uint32_t P, uint6
                 // --soak, profiles/r05/soak_bisect.txt).
                 __hip_atomic_store(reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(page)), h, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
-                if (out) st_nt(out + pg, h);
+                // the digest word an async stamp batch returns: system-scope
+                // too, since the host reads it as soon as the done byte lands
+                if (out) __hip_atomic_store(out + pg, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(ok + pg, (uint8_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
                 emit(MODE, pg, h, stored, const_cast<uint8_t*>(page), out, ok, nullptr);

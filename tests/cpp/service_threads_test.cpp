@@ -129,18 +129,19 @@ int run_validate(char* pool, int T, double secs, bool async, size_t max_n, std::
 }
 // --soak: see the header
 // PCS_SOAK_OPS / PCS_SOAK_CTL (bisecting aids, default all): bit masks of
-// the worker ops (1 sync validate, 2 async validate, 4 stamp) and of the
-// controller's actions (1 restarts, 2 gate flips, 4 torn drills, 8 re-post
-// drills).
+// the worker ops (1 sync validate, 2 async validate, 4 stamp, 8 async stamp
+// through pcs_batch, checking the digests it returns as well as the
+// headers) and of the controller's actions (1 restarts, 2 gate flips, 4 torn
+// drills, 8 re-post drills).
 int env_mask(const char* name, int dflt) {
     const char* v = std::getenv(name);
     return v && *v ? std::atoi(v) : dflt;
 }
 
 int soak(char* pool, int T, double secs) {
-    const int ops = env_mask("PCS_SOAK_OPS", 7), ctl = env_mask("PCS_SOAK_CTL", 15);
+    const int ops = env_mask("PCS_SOAK_OPS", 15), ctl = env_mask("PCS_SOAK_CTL", 15);
     std::vector<int> op_list;
-    for (int o = 0; o < 3; ++o)
+    for (int o = 0; o < 4; ++o)
         if (ops & (1 << o)) op_list.push_back(o);
     CHECK(!op_list.empty());
     std::atomic<int> errors{0};
@@ -163,20 +164,43 @@ int soak(char* pool, int T, double secs) {
         th.emplace_back([&, t] {
             uint64_t rng = 0x50A4ull + t * 104729ull;
             eloqstore::ChecksumBatch cb;
+            pcs_batch* sb = nullptr;  // async stamps with their digests
+            CHECK(pcs_batch_create(&sb) == PCS_OK);
             std::vector<uint8_t> ok;
+            std::vector<uint64_t> dig;
             while (!done.load(std::memory_order_relaxed)) {
                 const int op = op_list[splitmix(rng) % op_list.size()];
                 Req r = make_req(pool, t, rng, splitmix(rng) % 4 ? 24 : 256);
                 const auto t0 = Clock::now();
                 bool good = true;
-                if (op == 2) {  // stamp over zeroed headers
+                if (op >= 2) {  // stamp over zeroed headers (op 3: async, digests checked too)
                     std::vector<char*> w;
                     for (const char* p : r.ptrs) {
                         w.push_back(const_cast<char*>(p));
                         std::memset(w.back(), 0, 8);
                     }
                     const Counts s0 = counts();
-                    eloqstore::SetChecksums(w, P);
+                    if (op == 2) {
+                        eloqstore::SetChecksums(w, P);
+                    } else {
+                        CHECK(pcs_batch_submit(sb, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(w.data()), P,
+                                               w.size(), PCS_XXH3_64) == PCS_OK);
+                        int x;
+                        while ((x = pcs_batch_poll(sb)) == 0) {
+                        }
+                        CHECK(x == 1);
+                        dig.assign(w.size(), 0);
+                        CHECK(pcs_batch_result(sb, nullptr, dig.data(), nullptr) == PCS_OK);
+                        for (size_t i = 0; i < w.size(); ++i)
+                            if (dig[i] != oracle_page_xxh3(w[i], P)) {
+                                good = false;
+                                if (errors.load() < 12)
+                                    std::fprintf(stderr, "soak thread %d: async stamp n %zu page %zu: digest %016llx "
+                                                 "want %016llx\n", t, w.size(), i, (unsigned long long)dig[i],
+                                                 (unsigned long long)oracle_page_xxh3(w[i], P));
+                                break;
+                            }
+                    }
                     const Counts s1 = counts();
                     for (size_t i = 0; i < w.size(); ++i) {
                         uint64_t hdr;
@@ -226,6 +250,7 @@ int soak(char* pool, int T, double secs) {
                 if (!good && errors.fetch_add(1) < 5)
                     std::fprintf(stderr, "soak thread %d: op %d n %zu slot %zu wrong\n", t, op, r.ptrs.size(), r.k);
             }
+            pcs_batch_destroy(sb);
         });
     // the controller
     uint64_t rng = 0xC7A1ull;

@@ -378,17 +378,18 @@ def test_service_soak_under_restarts():
 
 def test_stamp_done_bytes_under_threads():
     """The launch path alone (no service): eight native threads stamping
-    small batches of their own zeroed pages, so every call completes from
-    per-page done bytes (zero-copy XXH3 stamps of up to
-    PCS_TUNE_ZC_STAMP_POLL_PAGES pages).  Every header must be in place when
-    SetChecksums returns.  With a non-temporal header store behind a release
+    small batches of their own zeroed pages, synchronously and through
+    pcs_batch, so every call completes from per-page done bytes (zero-copy
+    XXH3 stamps of up to PCS_TUNE_ZC_STAMP_POLL_PAGES pages).  Every header,
+    and every digest an async batch returns, must be in place when the call
+    returns.  With a non-temporal header store behind a release
     fence, ~1 header in 10^5 landed after its done byte
     (profiles/r05/soak_bisect_before_fix.txt); the header and the done byte
     are now system-scope stores."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(__file__), "cpp", "service_threads_test")
-    env = dict(os.environ, PCS_SOAK_OPS="4", PCS_SOAK_CTL="0", PCS_SOAK_START="off")
+    env = dict(os.environ, PCS_SOAK_OPS="12", PCS_SOAK_CTL="0", PCS_SOAK_START="off")
     r = subprocess.run([exe, "--soak", "6"], capture_output=True, text=True, timeout=100, env=env)
     assert r.returncode == 0 and "service soak ok" in r.stdout, r.stdout + r.stderr
     assert " 0 served" in r.stdout, r.stdout

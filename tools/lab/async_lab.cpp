@@ -49,6 +49,23 @@ int main() {
     std::vector<uint8_t> okw(8);
     uint64_t fbw;
     CHECK(pcs_pages_validate_host(warm.data(), P, 8, 0, okw.data(), &fbw) == PCS_OK);
+    // optionally run the gather path once (its three staging slots each make
+    // a stream, as in integration_snippets --crossover): with GPU_MAX_HW_QUEUES
+    // = 4 the process then has more streams than hardware queues
+    if (std::getenv("ASYNC_LAB_GATHER")) {
+        std::vector<char> heap(64 * P);
+        for (int i = 0; i < 64; ++i) {
+            oracle_fill_pages(heap.data() + i * P, P, 1, 0xBEEF, i);
+            oracle_set_checksum(heap.data() + i * P, P);
+        }
+        std::vector<const void*> hp(64);
+        for (int i = 0; i < 64; ++i) hp[i] = heap.data() + i * P;
+        std::vector<uint8_t> okh(64);
+        uint64_t fbh;
+        CHECK(pcs_pages_validate_host(hp.data(), P, 64, 0, okh.data(), &fbh) == PCS_OK && fbh == UINT64_MAX);
+        CHECK(pcs_counter(PCS_COUNTER_GATHER_CHUNKS) > 0);
+        std::printf("(gather path run first: its staging streams exist)\n");
+    }
     pcs_batch* b = nullptr;
     CHECK(pcs_batch_create(&b) == PCS_OK);
     std::mt19937_64 rng(7);
