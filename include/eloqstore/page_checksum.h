@@ -60,9 +60,11 @@ enum class PageHash : int { XXH3_64 = 0, XXH64 = 1 };
 // the columns in a fresh random order, with a control column that must agree
 // within 3 %; DESIGN.md §5, profiles/r05/crossover_r05e.txt):
 //   registered pool (RegisterPagePool, zero-copy): GPU faster from 32 pages
-//   to validate and to stamp (32 pages = 128 KiB);
-//   unregistered pages (gathered into staging):    GPU faster from 256 pages.
+//   to validate (32 pages = 128 KiB) and from 32-48 pages to stamp (three
+//   boxes: 32, 48, 48; the write gate is 48 pages = 192 KiB);
+//   unregistered pages (gathered into staging):    GPU faster from 192-256 pages.
 inline constexpr size_t kGpuChecksumMinBatchBytes = size_t(128) << 10;
+inline constexpr size_t kGpuStampMinBatchBytes = size_t(192) << 10;  // FlushBatchPages
 inline constexpr size_t kGpuChecksumMinBatchBytesStaged = size_t(1) << 20;
 inline bool GpuChecksumPays(size_t n_pages, size_t page_size, size_t min_bytes = kGpuChecksumMinBatchBytes) {
     return n_pages * page_size >= min_bytes;

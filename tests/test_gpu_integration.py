@@ -37,6 +37,9 @@ def test_integration_snippets_run():
     assert "write path append=1: 256 pages stamped (GPU batch)" in r.stdout
     assert "write path append=1: 10 pages stamped (reference loop)" in r.stdout
     assert "write path append=0: 40 pages stamped (reference loop)" in r.stdout
+    # between the read gate (32 pages) and the write gate (48): the loop; at 48: the GPU
+    assert "write path append=1: 40 pages stamped (reference loop)" in r.stdout
+    assert "write path append=1: 48 pages stamped (GPU batch)" in r.stdout
     assert "6-page scan batch on the reference loop" in r.stdout
     assert "read path with the validate service: ok (32 and 128 pages served, 6 on the reference loop" in r.stdout
     assert "async batch of 6 pages through the service: ok" in r.stdout
