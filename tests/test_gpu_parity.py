@@ -816,10 +816,12 @@ def test_huge_pages(P, n, algo):
 def test_xxh64_desc_sparse_offshape_pages():
     """XXH64 descriptor batch of 100,000 line-shaped 4 KiB pages with three
     off-shape pages (8-byte-aligned, lengths not a multiple of 64) at the
-    first, a middle and the last index: the LDS kernel flags the call, the
-    gated generic pass (one block per CU, grid-stride) picks exactly those
-    pages up; the same batch without them leaves the generic pass idle.
-    Digests against the oracle at the odd pages and a sample of the rest."""
+    first, a middle and the last index.  Since round 5 the LDS kernel hashes
+    them in place (the quad's first lane, any-size body): one launch per call.
+    Digests against the oracle at the odd pages and a sample of the rest;
+    then validate after a stamp, with one off-shape and one line-shaped page
+    corrupted and a 4-byte page (shorter than its header, never valid)
+    added: verdicts and first_bad exact."""
     n, P = 100_000, 4096
     lens = np.full(n, P, dtype=np.uint32)
     odd = [0, 51_234, n - 1]
@@ -851,3 +853,19 @@ def test_xxh64_desc_sparse_offshape_pages():
     got2 = u64(pcs.desc_digest(base2, d_off2, d_len2, n, pcs.XXH64))
     want2 = oracle.desc_digest(host[: n * P], offs2[check], lens2[check], pcs.XXH64)
     assert np.array_equal(got2[check], want2)
+    # validate: stamp the packed batch, corrupt an off-shape page (the middle
+    # one) and a line-shaped one after it, then shrink page 70,000 to 4 bytes
+    pcs.desc_stamp(base, d_off, d_len, n, pcs.XXH64)
+    ok, fb = pcs.desc_validate(base, d_off, d_len, n, pcs.XXH64)
+    assert int(ok.sum().item()) == n and int(fb.item()) == -1  # UINT64_MAX read as int64
+    b = base.cpu().numpy()
+    for i, byte in ((odd[1], 20), (60_000, 3000)):
+        b[int(offs[i]) + byte] ^= 0x40
+    lens3 = lens.copy()
+    lens3[70_000] = 4
+    base3 = torch.from_numpy(b).to(DEV)
+    d_len3 = torch.from_numpy(lens3.view(np.int32)).to(DEV)
+    ok, fb = pcs.desc_validate(base3, d_off, d_len3, n, pcs.XXH64)
+    bad = np.flatnonzero(ok.cpu().numpy() == 0).tolist()
+    assert bad == [odd[1], 60_000, 70_000], bad
+    assert int(fb.item()) == odd[1]
