@@ -50,6 +50,10 @@ Also reported, on the same line:
                 config 2 validate (read path) and stamp (write path), each with
                 its avg launch time, roofline frac, parity sample and
                 corruption drill.
+  sweep_multi   (N>1) the north star's 16 KiB (config 7 sizes) and 64 KiB
+                (config 4) page batches on every rank, weak scaling like the
+                headline: aggregate and per-GPU GiB/s, the aggregate roofline,
+                rank 0's launch time and frac, parity and drill per rank.
   scaling_detail (N>1) per-rank wall and kernel-event times, and
                 concurrent_over_solo = per-GPU rate / rank 0's rate on the same
                 shard run alone (an interference check; scaling efficiency is
@@ -721,6 +725,80 @@ def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale):
     return e
 
 
+def min_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+# N > 1: the north star's 16 KiB and 64 KiB page batches at every GPU count,
+# beside the 4 KiB headline (config 5): the same weak-scaling timing
+MULTI_SWEEP = (("config7_xxh3", 7), ("config4_xxh3", 4))
+
+
+def multi_rank_sweep(dist, world: int, rank: int, dev: str, algo: int, steps: int, warmup: int, scale: int):
+    """Each entry on every rank: its own shard of the config (global page
+    indices rank * n ...), `steps` launches timed between barriers, value =
+    bytes of all ranks / the max-over-ranks wall time, then parity and the
+    drill on every rank.  Every rank reaches every collective: a local
+    failure is recorded, never raised."""
+    out = []
+    for key, cfg in MULTI_SWEEP:
+        w, err = None, None
+        try:
+            w = Workload(cfg, algo, rank, max(1, CONFIGS[cfg][1] // scale), dev)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"[:300]
+        if min_over_ranks(dist, 0.0 if err else 1.0) < 1.0:
+            out.append({"key": key, "config": cfg, "error": err or "another rank failed to build its shard"})
+            w = None
+            continue
+        for _ in range(warmup):
+            w.step("digest")
+        torch.cuda.synchronize()
+        barrier(dist)
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for _ in range(steps):
+            w.step("digest")
+        ev1.record()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier(dist)
+        elapsed = max_over_ranks(dist, t1 - t0)
+        total = sum_over_ranks(dist, float(w.bytes)) * steps
+        avg = ev0.elapsed_time(ev1) / 1e3 / steps
+        try:
+            par = parity_sample(w)
+        except Exception as e:  # noqa: BLE001
+            par = {"error": f"{type(e).__name__}: {e}"[:300]}
+        try:
+            drill = w.corruption_drill()
+        except Exception as e:  # noqa: BLE001
+            drill = {"error": f"{type(e).__name__}: {e}"[:300], "pass": False}
+        checks, ok = gather_checks(dist, world, rank, par, drill)
+        value = total / elapsed / GIB
+        alg = w.algorithmic_bytes("digest")
+        out.append({"key": key, "config": cfg, "workload": w.desc, "pages_per_gpu": w.n, "bytes_per_gpu": w.bytes,
+                    "steps": steps, "warmup": warmup, "value": round(value, 2), "unit": "GiB/s",
+                    "per_gpu_GiBps": round(value / world, 2),
+                    "aggregate_roofline": {"GBps": round(value * GIB / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS * world,
+                                           "frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * world), 4)},
+                    "rank0_avg_launch_ms": round(avg * 1e3, 4) if rank == 0 else None,
+                    "rank0_frac": round(alg / avg / 1e9 / HBM_PEAK_GBPS, 4) if rank == 0 else None,
+                    "checks_all_ranks_pass": ok,
+                    "parity_per_rank": [dict(c["parity"], rank=c["rank"]) for c in checks],
+                    "drill_per_rank": [dict(c["corruption_drill"], rank=c["rank"]) for c in checks]})
+        w.free()
+        del w
+        time.sleep(PHASE_GAP_S)
+    return out
+
+
 def committed_traffic_key(key: str):
     """HBM bytes per launch for a sweep entry from the committed summary."""
     best = None
@@ -973,6 +1051,11 @@ def main():
     if args.host_inclusive and rank == 0:
         hostinc = guarded("host_inclusive", host_inclusive, w) if time.perf_counter() < deadline else \
             {"skipped": "bench wall budget spent"}
+    multi_entries = None
+    if world > 1 and not args.no_sweep:
+        multi_entries = multi_rank_sweep(dist, world, rank, dev, algo, args.sweep_steps, args.sweep_warmup,
+                                         max(1, args.sweep_scale))
+        checks_ok = checks_ok and all(e.get("checks_all_ranks_pass") for e in multi_entries)
     sweep_entries = None
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep_entries = guarded("sweep", sweep, dev, args.sweep_steps, args.sweep_warmup,
@@ -1059,12 +1142,16 @@ def main():
             line["host_inclusive"] = hostinc
         if sweep_entries is not None:
             line["sweep"] = sweep_entries
+        if multi_entries is not None:
+            line["sweep_multi"] = multi_entries
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     if not checks_ok:
         bad = [c["rank"] for c in per_rank_checks if not parity_ok(c["parity"], c["corruption_drill"])]
-        print(f"bench: parity or corruption drill failed on rank(s) {bad}", file=sys.stderr)
+        bad_sweep = [e["key"] for e in (multi_entries or []) if not e.get("checks_all_ranks_pass")]
+        print(f"bench: parity or corruption drill failed: headline rank(s) {bad}, sweep_multi {bad_sweep}",
+              file=sys.stderr)
         sys.exit(3)
 
 

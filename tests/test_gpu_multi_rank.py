@@ -105,7 +105,17 @@ def test_bench_two_ranks_torchrun():
     assert [p["rank"] for p in sd["per_rank"]] == [0, 1]
     assert all(p["kernel_event_ms_per_step"] > 0 and p["wall_s"] > 0 for p in sd["per_rank"])
     assert sd["concurrent_over_solo"] > 0 and sd["solo_rank0_GiBps"] > 0 and sd["shared_gpus"]
-    assert "sweep" not in line  # the sweep is an N=1 leg
+    assert "sweep" not in line  # the N=1 sweep
+    # the north star's 16 KiB and 64 KiB batches at N > 1, full sizes per rank
+    sm = line["sweep_multi"]
+    assert [e["key"] for e in sm] == ["config7_xxh3", "config4_xxh3"]
+    for e in sm:
+        assert "error" not in e, e
+        assert e["checks_all_ranks_pass"] and [p["rank"] for p in e["parity_per_rank"]] == [0, 1]
+        assert e["value"] > 0 and e["aggregate_roofline"]["peak_GBps"] == 2 * 8000.0 and 0 < e["rank0_frac"] < 1
+        n = e["pages_per_gpu"]
+        assert [p["global_pages"] for p in e["parity_per_rank"]] == [[0, n], [n, 2 * n]]
+    assert [e["bytes_per_gpu"] for e in sm] == [4 << 30, 16 << 30]
 
 
 def test_bench_four_ranks_torchrun():
@@ -114,7 +124,8 @@ def test_bench_four_ranks_torchrun():
     line, each over its own global range."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           "bench.py", "--gpus", "4", "--steps", "3", "--warmup", "1", "--pages-per-gpu", str(1 << 20)]
+           "bench.py", "--gpus", "4", "--steps", "3", "--warmup", "1", "--pages-per-gpu", str(1 << 20),
+           "--sweep-steps", "3", "--sweep-warmup", "1", "--sweep-scale", "16"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -125,3 +136,5 @@ def test_bench_four_ranks_torchrun():
     assert [p["global_pages"] for p in line["parity_per_rank"]] == [[r * n, (r + 1) * n] for r in range(4)]
     assert all(p["mismatches"] == 0 and p["content_mismatches"] == 0 for p in line["parity_per_rank"])
     assert [d["rank"] for d in line["drill_per_rank"]] == [0, 1, 2, 3] and all(d["pass"] for d in line["drill_per_rank"])
+    assert [e["key"] for e in line["sweep_multi"]] == ["config7_xxh3", "config4_xxh3"]
+    assert all(e["checks_all_ranks_pass"] and len(e["drill_per_rank"]) == 4 for e in line["sweep_multi"])
