@@ -816,8 +816,11 @@ def test_huge_pages(P, n, algo):
 def test_xxh64_desc_sparse_offshape_pages():
     """XXH64 descriptor batch of 100,000 line-shaped 4 KiB pages with three
     off-shape pages (8-byte-aligned, lengths not a multiple of 64) at the
-    first, a middle and the last index.  Since round 5 the LDS kernel hashes
-    them in place (the quad's first lane, any-size body): one launch per call.
+    first, a middle and the last index: the LDS kernel flags the call, the
+    gated generic pass (one block per CU, grid-stride) picks exactly those
+    pages up; the same batch without them leaves the generic pass idle.
+    (Round 5 measured hashing them inside the LDS kernel instead, one launch
+    per call, and kept the two launches: DESIGN.md §4.2.)
     Digests against the oracle at the odd pages and a sample of the rest;
     then validate after a stamp, with one off-shape and one line-shaped page
     corrupted and a 4-byte page (shorter than its header, never valid)
