@@ -970,10 +970,16 @@ def main():
         w.step("stamp")
         torch.cuda.synchronize()
 
+    # The trace's phase gap goes BEFORE the warmup, never between it and the
+    # timed steps: 0.1 s of idle GPU there cost the driver's short run
+    # (--steps 20 --warmup 5) 2.1 % (6,725 vs 6,872 GiB/s, medians of 10 in one
+    # process) and 0.15 % at 400 steps (tools/lab/bench_gap_lab.py,
+    # profiles/r05/bench_gap_r05y.txt): the part slows down while idle, and the
+    # warmup exists to bring it back before the clock starts.
+    time.sleep(PHASE_GAP_S)
     for _ in range(args.warmup):
         w.step(args.mode)
     torch.cuda.synchronize()
-    time.sleep(PHASE_GAP_S)
 
     # Two HIP events on the launch stream (torch's current stream) bracket the
     # K steps: the average launch duration is their span / K.  Events around
