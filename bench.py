@@ -616,6 +616,27 @@ def batch_latency(pool, pageable, w: Workload):
     return out
 
 
+SETTLE_MS = 200.0
+
+
+def settle(w: Workload, mode: str, ms: float) -> int:
+    """Untimed steps, in batches of 8, until at least `ms` of them have run;
+    returns how many.  The headline's timed region then starts on a part that
+    has left its idle state: a fresh process (or 0.1 s of idle) followed by
+    only the driver's 5 warmup steps (3 ms) timed 20 steps up to 2 % slow
+    (profiles/r05/bench_gap_r05y.txt)."""
+    if ms <= 0:
+        return 0
+    n = 0
+    t_end = time.perf_counter() + ms / 1e3
+    while n == 0 or time.perf_counter() < t_end:
+        for _ in range(8):
+            w.step(mode)
+        n += 8
+        torch.cuda.synchronize()
+    return n
+
+
 def timed_launches(w: Workload, mode: str, steps: int, warmup: int, rounds: int = 1) -> float:
     """Average launch time (s) of `steps` back-to-back steps, bracketed by two
     HIP events on the launch stream (torch's current stream).  With rounds >
@@ -930,6 +951,8 @@ def main():
                     help="take roofline.traffic from the committed profiles/ summary instead of two rocprofv3 "
                          "--pmc passes in this run")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--settle-ms", type=float, default=SETTLE_MS,
+                    help="untimed steps for at least this long before the W warmup steps (0: none)")
     ap.add_argument("--wall-budget", type=float, default=360.0,
                     help="seconds from start after which the optional legs (config 1, host-inclusive, "
                          "sweep entries) are skipped and recorded as such; the headline line always prints")
@@ -977,6 +1000,7 @@ def main():
     # profiles/r05/bench_gap_r05y.txt): the part slows down while idle, and the
     # warmup exists to bring it back before the clock starts.
     time.sleep(PHASE_GAP_S)
+    settle_steps = settle(w, args.mode, args.settle_ms)
     for _ in range(args.warmup):
         w.step(args.mode)
     torch.cuda.synchronize()
@@ -1093,6 +1117,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"ms": args.settle_ms, "steps": settle_steps},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
