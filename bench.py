@@ -686,7 +686,7 @@ PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits th
 
 
 def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale: int = 1,
-          deadline: float | None = None):
+          deadline: float | None = None, settle_ms: float = SETTLE_MS):
     """Each entry on a device-resident workload that stays allocated until the
     sweep ends: config 2 entries reuse the headline's batch (`head`), config 3
     XXH64 reuses config 3's arena.  Nothing is freed between entries: a
@@ -706,14 +706,14 @@ def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale
             out.append({"key": key, "config": cfg, "skipped": "bench wall budget spent"})
             continue
         try:
-            out.append(sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale))
+            out.append(sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale, settle_ms))
         except Exception as e:  # noqa: BLE001 — recorded in the line, never loses it
             out.append({"key": key, "config": cfg, "error": f"{type(e).__name__}: {e}"[:500]})
         time.sleep(PHASE_GAP_S)
     return out
 
 
-def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale):
+def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale, settle_ms=SETTLE_MS):
     """One sweep entry (see sweep())."""
     if cfg not in resident:
         resident[cfg] = Workload(cfg, algo, 0, max(1, CONFIGS[cfg][1] // scale), dev)
@@ -723,6 +723,7 @@ def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale):
         w.step("stamp")
     torch.cuda.synchronize()
     time.sleep(PHASE_GAP_S)
+    settle(w, mode, settle_ms)  # as the headline: the part leaves its idle state before the warmup
     t_wall0 = time.perf_counter()
     rounds = SWEEP_ROUNDS if steps >= 2 * SWEEP_ROUNDS else 1
     avg = timed_launches(w, mode, steps, warmup, rounds)
@@ -759,7 +760,8 @@ def min_over_ranks(dist, x: float) -> float:
 MULTI_SWEEP = (("config7_xxh3", 7), ("config4_xxh3", 4))
 
 
-def multi_rank_sweep(dist, world: int, rank: int, dev: str, algo: int, steps: int, warmup: int, scale: int):
+def multi_rank_sweep(dist, world: int, rank: int, dev: str, algo: int, steps: int, warmup: int, scale: int,
+                     settle_ms: float = SETTLE_MS):
     """Each entry on every rank: its own shard of the config (global page
     indices rank * n ...), `steps` launches timed between barriers, value =
     bytes of all ranks / the max-over-ranks wall time, then parity and the
@@ -776,6 +778,7 @@ def multi_rank_sweep(dist, world: int, rank: int, dev: str, algo: int, steps: in
             out.append({"key": key, "config": cfg, "error": err or "another rank failed to build its shard"})
             w = None
             continue
+        settle(w, "digest", settle_ms)
         for _ in range(warmup):
             w.step("digest")
         torch.cuda.synchronize()
@@ -1084,12 +1087,13 @@ def main():
     multi_entries = None
     if world > 1 and not args.no_sweep:
         multi_entries = multi_rank_sweep(dist, world, rank, dev, algo, args.sweep_steps, args.sweep_warmup,
-                                         max(1, args.sweep_scale))
+                                         max(1, args.sweep_scale), args.settle_ms)
         checks_ok = checks_ok and all(e.get("checks_all_ranks_pass") for e in multi_entries)
     sweep_entries = None
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep_entries = guarded("sweep", sweep, dev, args.sweep_steps, args.sweep_warmup,
-                                head=w if algo == 0 else None, scale=max(1, args.sweep_scale), deadline=deadline)
+                                head=w if algo == 0 else None, scale=max(1, args.sweep_scale), deadline=deadline,
+                                settle_ms=args.settle_ms)
     c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         all_s = None if args.no_all_cores else min(args.cpu_seconds, 5.0)
