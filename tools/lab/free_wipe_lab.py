@@ -1,0 +1,74 @@
+"""free_wipe_lab.py — is the GPU slower for a while after another process
+frees a lot of HBM (a driver-side wipe or clear of the freed memory)?
+
+    python tools/lab/free_wipe_lab.py hog GIB     allocate and fill GIB GiB, exit
+    python tools/lab/free_wipe_lab.py probe SECS  config-2 workload (1 M x 4 KiB
+        XXH3 digests): batches of 8 steps, each timed with HIP events, for
+        SECS seconds from the first batch; prints a time series of the
+        per-step time and a summary (first 200 ms, 0.2-1 s, the rest)
+
+tools/lab/r05_wipe.sh runs: probe alone; hog 80 GiB then probe at once; hog
+then 5 s of sleep then probe.
+"""
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
+
+import torch  # noqa: E402
+
+
+def hog(gib: float):
+    bufs = []
+    left = int(gib * (1 << 30))
+    while left > 0:
+        b = min(left, 8 << 30)
+        t = torch.empty(b, dtype=torch.uint8, device="cuda:0")
+        t.fill_(0x5A)
+        bufs.append(t)
+        left -= b
+    torch.cuda.synchronize()
+    print(f"hog: {gib} GiB allocated and filled", flush=True)
+
+
+def probe(secs: float):
+    import bench
+    import eloqstore_amd as pcs
+    t_proc = time.perf_counter()
+    if pcs.lib().pcs_set_device(0) != 0:
+        raise SystemExit("pcs_set_device failed")
+    w = bench.Workload(2, pcs.XXH3_64, 0, None, "cuda:0")
+    t_ready = time.perf_counter()
+    series = []
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < secs:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(8):
+            w.step("digest")
+        e1.record()
+        torch.cuda.synchronize()
+        series.append(((time.perf_counter() - t0) * 1e3, e0.elapsed_time(e1) * 1e3 / 8))
+    print(f"probe: workload ready {t_ready - t_proc:.2f} s after start; {len(series)} batches", flush=True)
+    for t, us in series[:12] + series[12::25]:
+        print(f"  t={t:8.1f} ms  {us:7.1f} us/step", flush=True)
+    best = min(us for _, us in series)
+
+    def seg(a, b):
+        v = [us for t, us in series if a <= t < b]
+        return (statistics.median(v), max(v), len(v)) if v else (float("nan"), float("nan"), 0)
+
+    for a, b in ((0, 200), (200, 1000), (1000, 1e9)):
+        m, mx, k = seg(a, b)
+        print(f"SEG {a:>5}-{'end' if b > 1e8 else int(b):>5} ms: median {m:7.1f} us/step ({m / best:.4f} x best), "
+              f"max {mx:7.1f}, {k} batches", flush=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "hog":
+        hog(float(sys.argv[2]))
+    else:
+        probe(float(sys.argv[2]))
