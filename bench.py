@@ -616,15 +616,19 @@ def batch_latency(pool, pageable, w: Workload):
     return out
 
 
-SETTLE_MS = 200.0
+SETTLE_MS = 1500.0       # the headline, at the start of the process
+SWEEP_SETTLE_MS = 200.0  # each sweep entry, later in the same process
 
 
 def settle(w: Workload, mode: str, ms: float) -> int:
     """Untimed steps, in batches of 8, until at least `ms` of them have run;
-    returns how many.  The headline's timed region then starts on a part that
-    has left its idle state: a fresh process (or 0.1 s of idle) followed by
-    only the driver's 5 warmup steps (3 ms) timed 20 steps up to 2 % slow
-    (profiles/r05/bench_gap_r05y.txt)."""
+    returns how many.  The timed region then starts on a part in its steady
+    state.  A fresh process (or 0.1 s of idle) followed by only the driver's
+    5 warmup steps (3 ms) timed 20 steps up to 2 % slow
+    (profiles/r05/bench_gap_r05y.txt), and for up to ~1 s after a process
+    starts -- after another process that used (and freed) a lot of HBM has
+    exited, and on some fresh boxes -- steps run ~2 % slower than from then on
+    (tools/lab/free_wipe_lab.py, profiles/r05/free_wipe_r05y.txt)."""
     if ms <= 0:
         return 0
     n = 0
@@ -686,7 +690,7 @@ PHASE_GAP_S = 0.1  # idle gap between phases: tools/summarize_sweep.py splits th
 
 
 def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale: int = 1,
-          deadline: float | None = None, settle_ms: float = SETTLE_MS):
+          deadline: float | None = None, settle_ms: float = SWEEP_SETTLE_MS):
     """Each entry on a device-resident workload that stays allocated until the
     sweep ends: config 2 entries reuse the headline's batch (`head`), config 3
     XXH64 reuses config 3's arena.  Nothing is freed between entries: a
@@ -713,7 +717,7 @@ def sweep(dev: str, steps: int, warmup: int, head: Workload | None = None, scale
     return out
 
 
-def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale, settle_ms=SETTLE_MS):
+def sweep_entry(key, cfg, algo, mode, resident, dev, steps, warmup, scale, settle_ms=SWEEP_SETTLE_MS):
     """One sweep entry (see sweep())."""
     if cfg not in resident:
         resident[cfg] = Workload(cfg, algo, 0, max(1, CONFIGS[cfg][1] // scale), dev)
@@ -761,7 +765,7 @@ MULTI_SWEEP = (("config7_xxh3", 7), ("config4_xxh3", 4))
 
 
 def multi_rank_sweep(dist, world: int, rank: int, dev: str, algo: int, steps: int, warmup: int, scale: int,
-                     settle_ms: float = SETTLE_MS):
+                     settle_ms: float = SWEEP_SETTLE_MS):
     """Each entry on every rank: its own shard of the config (global page
     indices rank * n ...), `steps` launches timed between barriers, value =
     bytes of all ranks / the max-over-ranks wall time, then parity and the
@@ -1087,13 +1091,13 @@ def main():
     multi_entries = None
     if world > 1 and not args.no_sweep:
         multi_entries = multi_rank_sweep(dist, world, rank, dev, algo, args.sweep_steps, args.sweep_warmup,
-                                         max(1, args.sweep_scale), args.settle_ms)
+                                         max(1, args.sweep_scale), min(args.settle_ms, SWEEP_SETTLE_MS))
         checks_ok = checks_ok and all(e.get("checks_all_ranks_pass") for e in multi_entries)
     sweep_entries = None
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep_entries = guarded("sweep", sweep, dev, args.sweep_steps, args.sweep_warmup,
                                 head=w if algo == 0 else None, scale=max(1, args.sweep_scale), deadline=deadline,
-                                settle_ms=args.settle_ms)
+                                settle_ms=min(args.settle_ms, SWEEP_SETTLE_MS))
     c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         all_s = None if args.no_all_cores else min(args.cpu_seconds, 5.0)

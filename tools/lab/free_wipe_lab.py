@@ -5,7 +5,7 @@ frees a lot of HBM (a driver-side wipe or clear of the freed memory)?
     python tools/lab/free_wipe_lab.py probe SECS  config-2 workload (1 M x 4 KiB
         XXH3 digests): batches of 8 steps, each timed with HIP events, for
         SECS seconds from the first batch; prints a time series of the
-        per-step time and a summary (first 200 ms, 0.2-1 s, the rest)
+        per-step time, the device's free memory (hipMemGetInfo) and a summary (first 200 ms, 0.2-1 s, the rest)
 
 tools/lab/r05_wipe.sh runs: probe alone; hog 80 GiB then probe at once; hog
 then 5 s of sleep then probe.
@@ -51,14 +51,15 @@ def probe(secs: float):
             w.step("digest")
         e1.record()
         torch.cuda.synchronize()
-        series.append(((time.perf_counter() - t0) * 1e3, e0.elapsed_time(e1) * 1e3 / 8))
+        free = torch.cuda.mem_get_info(0)[0]
+        series.append(((time.perf_counter() - t0) * 1e3, e0.elapsed_time(e1) * 1e3 / 8, free))
     print(f"probe: workload ready {t_ready - t_proc:.2f} s after start; {len(series)} batches", flush=True)
-    for t, us in series[:12] + series[12::25]:
-        print(f"  t={t:8.1f} ms  {us:7.1f} us/step", flush=True)
-    best = min(us for _, us in series)
+    for t, us, free in series[:12] + series[12::25]:
+        print(f"  t={t:8.1f} ms  {us:7.1f} us/step  free {free / 2**30:8.2f} GiB", flush=True)
+    best = min(us for _, us, _ in series)
 
     def seg(a, b):
-        v = [us for t, us in series if a <= t < b]
+        v = [us for t, us, _ in series if a <= t < b]
         return (statistics.median(v), max(v), len(v)) if v else (float("nan"), float("nan"), 0)
 
     for a, b in ((0, 200), (200, 1000), (1000, 1e9)):
