@@ -103,9 +103,22 @@ def dist_env():
 
 
 def init_dist(world: int):
+    """gloo for the barrier and the max/sum over ranks (no data-path
+    collective).  gloo's connection messages ("[Gloo] Rank r is connected to
+    ...") are written to stdout by the C++ library; they are moved to stderr
+    here so that stdout carries only rank 0's JSON line."""
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        sys.stdout.flush()
+        saved = os.dup(1)
+        try:
+            os.dup2(2, 1)
+            dist.init_process_group("gloo")
+            dist.barrier()  # every rank connected before stdout is restored
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         return dist
     return None
 

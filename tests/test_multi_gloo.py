@@ -76,3 +76,33 @@ def test_rank_shards_match_single_process(tmp_path, world):
     mx, sm = open(tmp_path / "stats.txt").read().split()
     assert float(mx) == world and float(sm) == N_PAGES
     assert open(tmp_path / "checks.txt").read().strip() == f"{list(range(world))} False [1]"
+
+
+GLOO_STDOUT_SCRIPT = r'''
+import sys
+sys.path.insert(0, {root!r})
+import bench
+world, rank, local = bench.dist_env()
+dist = bench.init_dist(world)
+mx = bench.max_over_ranks(dist, float(rank))
+bench.barrier(dist)
+if rank == 0:
+    print('{{"max_rank": %d}}' % mx, flush=True)
+'''
+
+
+def test_init_dist_keeps_stdout_to_the_json_line(tmp_path):
+    """Under torch.distributed.run, gloo's C++ connection messages go to
+    stdout by default; bench.init_dist moves them to stderr, so the driver
+    reads exactly one line (rank 0's JSON) from a multi-rank bench run."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "gloo_stdout.py"
+    script.write_text(GLOO_STDOUT_SCRIPT.format(root=root))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(script)],
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines() == ['{"max_rank": 2}'], r.stdout
