@@ -86,7 +86,7 @@ def test_bench_two_ranks_torchrun():
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-3000:]  # rank 0 only
+    assert len(lines) == 1 and r.stdout.strip().splitlines() == lines, r.stdout[-3000:]  # rank 0 only, nothing else
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 3
     assert line["config"]["workload"].startswith("config5")
@@ -129,7 +129,7 @@ def test_bench_four_ranks_torchrun():
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-3000:]
+    assert len(lines) == 1 and r.stdout.strip().splitlines() == lines, r.stdout[-3000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 4 and line["checks_all_ranks_pass"] is True
     n = 1 << 20
