@@ -68,8 +68,47 @@ def probe(secs: float):
               f"max {mx:7.1f}, {k} batches", flush=True)
 
 
+def series_of(w, secs):
+    out, t0 = [], time.perf_counter()
+    while time.perf_counter() - t0 < secs:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(8):
+            w.step("digest")
+        e1.record()
+        torch.cuda.synchronize()
+        out.append(((time.perf_counter() - t0) * 1e3, e0.elapsed_time(e1) * 1e3 / 8))
+    return out
+
+
+def probe2(secs: float):
+    """Is the slow phase tied to the process or to fresh allocations?  One
+    process: batch A for `secs`, then a freshly allocated batch B for `secs`,
+    then A again; per phase the median step time in 0-200 ms, 0.2-1 s and
+    the rest."""
+    import bench
+    import eloqstore_amd as pcs
+    if pcs.lib().pcs_set_device(0) != 0:
+        raise SystemExit("pcs_set_device failed")
+    a = bench.Workload(2, pcs.XXH3_64, 0, None, "cuda:0")
+    phases = [("A", series_of(a, secs))]
+    b = bench.Workload(2, pcs.XXH3_64, 0, None, "cuda:0")
+    phases.append(("B fresh", series_of(b, secs)))
+    phases.append(("A again", series_of(a, secs)))
+    best = min(us for _, s in phases for _, us in s)
+    for name, s in phases:
+        segs = []
+        for lo, hi in ((0, 200), (200, 1000), (1000, 1e9)):
+            v = [us for t, us in s if lo <= t < hi]
+            segs.append(f"{statistics.median(v):7.1f}" if v else "      -")
+        print(f"PHASE {name:8s} median us/step 0-200 ms {segs[0]}, 0.2-1 s {segs[1]}, rest {segs[2]} "
+              f"(best {best:.1f})", flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "hog":
         hog(float(sys.argv[2]))
+    elif sys.argv[1] == "probe2":
+        probe2(float(sys.argv[2]))
     else:
         probe(float(sys.argv[2]))
