@@ -68,3 +68,24 @@ def test_fill_pages_at_matches_contiguous_generator():
     idx = np.array([5, 0, 4096, 77, 8191], dtype=np.int64)
     whole = fill_pages(0x5EED0005, 0, 8192, 256)
     assert np.array_equal(fill_pages_at(0x5EED0005, idx, 256), whole[idx])
+
+
+def test_settle_runs_whole_batches_for_at_least_the_time(monkeypatch):
+    """bench.settle: untimed steps in batches of 8, synchronised after each
+    batch, until at least `ms` have passed; 0 ms runs nothing."""
+    import time
+
+    calls = {"step": 0, "sync": 0}
+
+    class FakeWorkload:
+        def step(self, mode):
+            assert mode == "digest"
+            calls["step"] += 1
+            time.sleep(0.0005)
+
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda: calls.__setitem__("sync", calls["sync"] + 1))
+    assert bench.settle(FakeWorkload(), "digest", 0) == 0 and calls["step"] == 0
+    t0 = time.perf_counter()
+    n = bench.settle(FakeWorkload(), "digest", 30)
+    assert time.perf_counter() - t0 >= 0.030
+    assert n == calls["step"] and n % 8 == 0 and n >= 8 and calls["sync"] == n // 8
