@@ -345,7 +345,10 @@ __device__ __forceinline__ uint64_t xxh64_quad_merge(uint64_t v) {
 // Page convention: XXH64 over [8, P).  Needs 8-byte aligned page, P % 8 == 0,
 // P >= 40 (so the hashed length is >= 32 and the 4-accumulator loop runs).
 constexpr int kX64Unroll = 16;
-constexpr int kX64LdsDepth = 2;  // segments in flight per LDS-kernel step (profiles/r01/x64_depth_lab.txt)
+// Segments in flight per LDS-kernel step (profiles/r01/x64_depth_lab.txt).  Round 5
+// (profiles/r05/x64_depth3_lab_r05z.txt): depth 3 (124 VGPRs, 4 waves per SIMD)
+// is -3.2 % on config 3 and +0.9 % on config 2, depth 4 -10.3 % / +0.5 %; 2 stays.
+constexpr int kX64LdsDepth = 2;
 template <bool NT>
 __device__ __forceinline__ uint64_t ld8(const uint64_t* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -1432,7 +1435,7 @@ constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, fa
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
                                       false, true,  false, false, false, true,  false, false, true};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
-                                          /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4 -> 1/2/4)*/ 0,
+                                          /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4/5 -> 1/2/4/3)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
                                           /*xxh3 split pages from this size (0 = never)*/ 8192,
                                           /*retired*/ 0,
@@ -1493,14 +1496,14 @@ bool split_pages(uint64_t P) {
 bool rt_batch4() { return g_tune[8].load(std::memory_order_relaxed) != 0; }
 
 // XXH64 LDS kernel launch with the segment depth from PCS_TUNE_XXH64_LAYOUT
-// (0 or 1 = default depth, 2/3/4 = depth 1/2/4) and the waves per workgroup
+// (0 or 1 = default depth, 2/3/4/5 = depth 1/2/4/3) and the waves per workgroup
 // from PCS_TUNE_XXH64_WAVES.
 template <int MODE, bool NT, int ADDR>
 void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const uint64_t* off, const uint32_t* len,
                       uint32_t P, uint64_t n, uint64_t* out, uint8_t* ok, unsigned long long* fb,
                       unsigned long long* offshape = nullptr, uint64_t call_id = 0) {
     const int64_t lay = g_tune[6].load(std::memory_order_relaxed);
-    const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : kX64LdsDepth;
+    const int depth = lay == 2 ? 1 : lay == 3 ? 2 : lay == 4 ? 4 : lay == 5 ? 3 : kX64LdsDepth;
     const int64_t wpb = g_tune[15].load(std::memory_order_relaxed);
     if (wpb == 1 || wpb == 2) {
         // one workgroup per 16 * wpb pages, every tile covered once
@@ -1509,10 +1512,12 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
         if (wpb == 1) {
             if (depth == 1) LW(1, 1);
             else if (depth == 2) LW(2, 1);
+            else if (depth == 3) LW(3, 1);
             else LW(4, 1);
         } else {
             if (depth == 1) LW(1, 2);
             else if (depth == 2) LW(2, 2);
+            else if (depth == 3) LW(3, 2);
             else LW(4, 2);
         }
 #undef LW
@@ -1521,6 +1526,7 @@ void launch_xxh64_lds(unsigned grid, hipStream_t s, const uint8_t* base, const u
 #define L(D) hipLaunchKernelGGL((k_xxh64_lds<MODE, NT, ADDR, D>), dim3(grid), dim3(kBlock), 0, s, base, off, len, P, n, out, ok, fb, offshape, call_id)
     if (depth == 1) L(1);
     else if (depth == 2) L(2);
+    else if (depth == 3) L(3);
     else L(4);
 #undef L
 }

@@ -267,7 +267,7 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     default cache policy (0)
  *   PCS_TUNE_XXH64_LAYOUT         [0] segments in flight per XXH64 LDS-kernel
  *                                     step: 0 or 1 = default (2), 2 -> 1,
- *                                     3 -> 2, 4 -> 4
+ *                                     3 -> 2, 4 -> 4, 5 -> 3
  *   PCS_TUNE_ZERO_COPY            [1] host batches over registered pages:
  *                                     1 = zero-copy (one launch, pages read in
  *                                     place); 0 = stage through device memory
