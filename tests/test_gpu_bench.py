@@ -34,6 +34,8 @@ def test_bench_line_and_sweep():
     assert d["parity"]["mismatches"] == 0 and d["parity"]["pages"] > 0
     assert d["corruption_drill"]["pass"]
     assert d["stream_read_GBps"] > 0
+    # untimed steps ran for the default 1.5 s before the warmup
+    assert d["settle"]["ms"] == 1500.0 and d["settle"]["steps"] >= 8 and d["settle"]["steps"] % 8 == 0
     assert [e["key"] for e in d["sweep"]] == SWEEP_KEYS
     for e in d["sweep"]:
         assert e["avg_launch_ms"] > 0 and 0 < e["frac"] < 1.0, e
