@@ -82,6 +82,8 @@ _SIGS = {
     "pcs_service_start_ex": [_i32, _i32, _u32],
     "pcs_service_stop": [],
     "pcs_service_running": [],
+    "pcs_last_path": [],
+    "pcs_batch_path": [_vp],
     "pcs_version": [],
     "pcs_abi_version": [],
     "pcs_last_error": [],
@@ -164,6 +166,15 @@ TUNE_FAIL_INJECT = 27  # test only
 TUNE_SERVICE_MAX_CALLERS = 28
 TUNE_SERVICE_REPOST_TEST = 30  # test only
 TUNE_ZC_STAMP_POLL_PAGES = 31
+TUNE_SERVICE_SLOW_EXIT_TEST = 33  # test only
+
+# PCS_PATH_* bits (pcs_last_path / pcs_batch_path)
+PATH_SERVED = 1
+PATH_LAUNCHED = 2
+PATH_FALLBACK = 4
+PATH_REPOSTED = 8
+PATH_NEW_GENERATION = 16
+PATH_LOCK_SKIPPED = 32
 
 COUNTER_ZERO_COPY_LAUNCHES = 0
 COUNTER_DIRECT_DMA_CHUNKS = 1
@@ -190,7 +201,7 @@ def version() -> str:
     return lib().pcs_version().decode()
 
 
-ABI_VERSION = 5  # PCS_ABI_VERSION of include/eloqstore_pcs.h this binding was written for
+ABI_VERSION = 6  # PCS_ABI_VERSION of include/eloqstore_pcs.h this binding was written for
 
 
 def abi_version() -> int:
@@ -335,6 +346,10 @@ class Batch:
 
     def wait(self) -> None:
         _call("pcs_batch_wait", self._b)
+
+    def path(self) -> int:
+        """PCS_PATH_* bits of the last submission (which path served it)."""
+        return int(lib().pcs_batch_path(self._b))
 
     def result(self):
         fb = ctypes.c_uint64(0)

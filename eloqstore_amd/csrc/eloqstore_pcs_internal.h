@@ -108,8 +108,9 @@ __host__ __device__ inline uint64_t service_word_mix(uint64_t w, uint64_t i) {
 // workgroup w serving line w / wpl.  Each serves its line's requests of that
 // generation until idle_ticks pass without one or, between requests, it has
 // lived life_ticks (both on the 100 MHz real-time clock), or stop is set, or
-// the box names a newer generation.
+// the box names a newer generation.  exit_ticks: test only (a kernel that
+// serves nothing and leaves that many ticks late; 0 in production).
 hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                       hipStream_t s);
+                       uint64_t exit_ticks, hipStream_t s);
 
 }  // namespace pcs

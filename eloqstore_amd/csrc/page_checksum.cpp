@@ -115,6 +115,8 @@ int ChecksumBatch::Collect() {
     return PCS_OK;
 }
 
+int ChecksumBatch::Path() const { return batch_ ? pcs_batch_path(batch_) : 0; }
+
 int ChecksumBatch::TryPoll() {
     if (status_) return status_;
     const int rc = pcs_batch_poll(batch_);

@@ -541,13 +541,25 @@ int host_batch(int mode, const void* const* pages, uint64_t P, uint64_t n, int a
 // of the process, so an asynchronous request still in flight when the
 // service stops can never read freed memory: it finds the service off and
 // re-runs its pages on the launch path.
+//
+// Nothing waits on the GPU while holding the service's lock (VERDICT r05 #1:
+// a poll on a shard thread must never stall behind another thread's stop).
+// Stopping or giving up on the kernels *retires* them: the box names a
+// generation no kernel serves, so every queued workgroup leaves at its next
+// poll, and an event recorded behind them says when they have.  pcs_service_stop
+// waits on that event after releasing the lock; a request that gives up on a
+// kernel that has not left (no answer in 5 s) quarantines its line until that
+// kernel's event completes, so no late verdict store can land in a later
+// request's words.  The poll path takes the lock with try_lock only.
 constexpr int kServiceEvents = 16;  // ring of events, one per generation (gen % 16)
 struct Service {
     using clock = std::chrono::steady_clock;
     struct Line {
-        std::atomic<int> owner{0};  // 1 while a request owns the line
+        std::atomic<int> owner{0};  // 0 free, 1 owned by a request, 2 quarantined (service_release)
         uint32_t count = 0;         // requests posted on it (low half of seq)
-        clock::time_point answered;  // when its last request was answered (>= its workgroups' idle clock)
+        // when its last request was answered (>= its workgroups' idle clock), steady-clock ticks
+        std::atomic<clock::rep> answered{0};
+        std::atomic<uint32_t> fence{0};  // quarantined: the generation whose kernel must leave first
     };
     std::mutex mu;                 // everything below except the atomics; never held while waiting
     std::atomic<int> callers{0};   // eligible calls in progress on this device, on either path
@@ -597,9 +609,11 @@ int service_launch_locked(Service& sv) {
     sv.gen.store(g, std::memory_order_release);
     sv.live = true;
     sv.launched = Service::clock::now();
-    for (int k = 0; k < sv.lines; ++k) sv.line[k].answered = sv.launched;
+    for (int k = 0; k < sv.lines; ++k)
+        sv.line[k].answered.store(sv.launched.time_since_epoch().count(), std::memory_order_relaxed);
+    const uint64_t exit_ticks = (uint64_t)std::max<int64_t>(0, pcs::get_tuning(PCS_TUNE_SERVICE_SLOW_EXIT_TEST)) * 100;
     hipError_t e = pcs::run_service(sv.d, sv.lines, sv.wpl, g, (uint64_t)sv.idle_us * 100,
-                                    (uint64_t)sv.idle_us * 200, sv.stream);
+                                    (uint64_t)sv.idle_us * 200, exit_ticks, sv.stream);
     if (e == hipSuccess) e = hipEventRecord(sv.done[g % kServiceEvents], sv.stream);
     return finish(e, "service kernel launch");
 }
@@ -609,8 +623,10 @@ int service_launch_locked(Service& sv) {
 // bounds the kernel's clocks).
 bool service_waiting(const Service& sv, int k, Service::clock::time_point now) {
     const auto margin = std::chrono::microseconds(sv.idle_us / 4);
+    const Service::clock::time_point answered{
+        Service::clock::duration(sv.line[k].answered.load(std::memory_order_relaxed))};
     return sv.live && now - sv.launched < std::chrono::microseconds(2 * (uint64_t)sv.idle_us) - margin &&
-           now - sv.line[k].answered < std::chrono::microseconds(sv.idle_us) - margin;
+           now - answered < std::chrono::microseconds(sv.idle_us) - margin;
 }
 
 // The check word of line `ln`'s request words as they now stand, with `seq`
@@ -634,37 +650,51 @@ uint64_t service_post_locked(Service& sv, int k, uint32_t gen) {
     return seq;
 }
 
-// Wait (bounded) until every kernel queued on `s` has left.
-hipError_t drain_bounded(hipStream_t s, std::chrono::milliseconds limit) {
+// Wait (bounded, outside every lock) until `ev` has completed.
+hipError_t event_wait_bounded(hipEvent_t ev, std::chrono::milliseconds limit) {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
-        const hipError_t q = hipStreamQuery(s);
+        const hipError_t q = hipEventQuery(ev);
         if (q != hipErrorNotReady) return q;
         if (std::chrono::steady_clock::now() - t0 > limit) return hipErrorNotReady;
         std::this_thread::yield();
     }
 }
 
-// End every queued kernel (stop word, then a bounded drain) so none can still
-// read a request line when it is next rewritten; the next request starts a
-// new generation.
-hipError_t service_reset_locked(Service& sv) {
-    __atomic_store_n(&sv.h->stop, 1, __ATOMIC_RELEASE);
-    const hipError_t e = drain_bounded(sv.stream, std::chrono::milliseconds(2000));
-    __atomic_store_n(&sv.h->stop, 0, __ATOMIC_RELEASE);
+// Retire every queued kernel without waiting for it: the box names
+// generation g + 1, which no kernel serves, so each workgroup leaves at its
+// next poll, and done[(g + 1) % 16], recorded behind them all, completes once
+// every one has.  The next request starts generation g + 2.  Returns that
+// event's generation.
+uint32_t service_retire_locked(Service& sv, hipError_t* err) {
+    const uint32_t g = sv.gen.load(std::memory_order_relaxed) + 1;
+    __atomic_store_n(&sv.h->gen, (uint64_t)g, __ATOMIC_RELEASE);
+    sv.gen.store(g, std::memory_order_release);
     sv.live = false;
-    return e;
+    const hipError_t e = hipEventRecord(sv.done[g % kServiceEvents], sv.stream);
+    if (err) *err = e;
+    return g;
 }
 
-int service_stop_locked(Service& sv) {
+// Turn the service off and retire its kernels under the lock, then wait for
+// them to leave (bounded) after releasing it.
+int service_stop(Service& sv) {
+    std::unique_lock<std::mutex> lk(sv.mu);
     if (sv.device < 0) return PCS_OK;
     g_services_on.fetch_sub(1, std::memory_order_relaxed);
     int cur = -1;
     const bool other = hipGetDevice(&cur) == hipSuccess && cur != sv.device;
     if (other) (void)hipSetDevice(sv.device);
     sv.device = -1;  // a request in flight now re-runs on the launch path
-    const hipError_t e = service_reset_locked(sv);
+    hipError_t e = hipSuccess;
+    const uint32_t g = service_retire_locked(sv, &e);
+    hipEvent_t ev = sv.done[g % kServiceEvents];
     if (other) (void)hipSetDevice(cur);
+    lk.unlock();
+    if (e != hipSuccess) return hip_fail(e, "service stop");
+    // A later generation re-recording this ring slot meanwhile only makes the
+    // wait longer: it completes after ours.
+    e = event_wait_bounded(ev, std::chrono::milliseconds(2000));
     if (e == hipErrorNotReady) return fail(PCS_ERR_HIP, "service stop: kernels did not leave within 2 s");
     return finish(e, "service stop");
 }
@@ -673,10 +703,15 @@ int service_stop_locked(Service& sv) {
 // runtime tears down (handlers registered after the runtime's first use run
 // before its own destructors).
 void service_at_exit() {
-    for (Service& sv : g_services) {
-        std::lock_guard<std::mutex> lk(sv.mu);
-        (void)service_stop_locked(sv);
-    }
+    for (Service& sv : g_services) (void)service_stop(sv);
+}
+
+// A quarantined line may be claimed again once the kernel of its fence
+// generation has left (its event; a newer generation's record in the same
+// ring slot completes later still, so this never clears a line too early).
+bool line_fence_passed(const Service& sv, int k) {
+    hipEvent_t ev = sv.done[sv.line[k].fence.load(std::memory_order_acquire) % kServiceEvents];
+    return ev && hipEventQuery(ev) == hipSuccess;
 }
 
 // The calling thread's device's service slot, or null.
@@ -766,12 +801,23 @@ struct ServiceReq {
     uint32_t gen = 0;       // the generation it is posted to
     bool stamp = false;
     int relaunched = 0;
+    int path = 0;           // PCS_PATH_* bits gathered so far
+    bool quarantine = false;  // given up while its generation's kernel may still run
     Service::clock::time_point posted, checked;
 };
 
+// Release the request's line: free, or quarantined until the kernel of the
+// request's generation has left when the request gave up on it before then
+// (a workgroup of it may still store a verdict into the line).
 void service_release(ServiceReq& r) {
     if (!r.sv) return;
-    r.sv->line[r.k].owner.store(0, std::memory_order_release);
+    Service::Line& l = r.sv->line[r.k];
+    if (r.quarantine) {
+        l.fence.store(r.gen, std::memory_order_relaxed);
+        l.owner.store(2, std::memory_order_release);
+    } else {
+        l.owner.store(0, std::memory_order_release);
+    }
     r.sv = nullptr;
 }
 
@@ -812,8 +858,9 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
     const int h0 = t_line_hint >= 0 ? t_line_hint : 0;
     for (int i = 0; i < nl && k < 0; ++i) {
         const int c = (h0 + i) % nl;
-        int expect = 0;
-        if (sv.line[c].owner.load(std::memory_order_relaxed) == 0 &&
+        const int o = sv.line[c].owner.load(std::memory_order_relaxed);
+        int expect = o;
+        if ((o == 0 || (o == 2 && line_fence_passed(sv, c))) &&
             sv.line[c].owner.compare_exchange_strong(expect, 1, std::memory_order_acquire))
             k = c;
     }
@@ -838,12 +885,14 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
     r.n = n;
     r.stamp = stamp;
     for (uint64_t i = 0; i < n; ++i) ln->ok[i] = pcs::kServicePending;
-    if (!service_waiting(sv, k, Service::clock::now()))
+    if (!service_waiting(sv, k, Service::clock::now())) {
         if (int rc = service_launch_locked(sv)) {
-            (void)service_reset_locked(sv);
+            (void)service_retire_locked(sv, nullptr);  // nothing was posted: the line is free again
             service_release(r);
             return rc;
         }
+        r.path |= PCS_PATH_NEW_GENERATION;
+    }
     const uint64_t page_word = P | (stamp ? pcs::kServiceStamp : 0);
     if (tear_us > 0) {
         // seq first, the request words after it, the check word last: until
@@ -888,18 +937,29 @@ int service_progress(ServiceReq& r) {
     const auto now = Service::clock::now();
     if (now - r.checked < std::chrono::microseconds(50) && r.gen == sv.gen.load(std::memory_order_acquire)) return 0;
     r.checked = now;
-    std::lock_guard<std::mutex> lk(sv.mu);
+    // Never wait for the lock: its holder (another thread's submit, start,
+    // stop or re-post) holds it for a launch at most, and this request is
+    // looked at again on the next call.
+    std::unique_lock<std::mutex> lk(sv.mu, std::try_to_lock);
+    if (!lk.owns_lock()) {
+        r.path |= PCS_PATH_LOCK_SKIPPED;
+        return 0;
+    }
     // Has the kernel of the generation this request was posted to left?  (Its
     // event; a newer generation's event in the same ring slot is later on
     // the stream, so its completion implies this one's.)
     const hipError_t q = hipEventQuery(sv.done[r.gen % kServiceEvents]);
     if (q == hipErrorNotReady) {
         if (now - r.posted < std::chrono::seconds(5)) return 0;
-        (void)service_reset_locked(sv);  // no answer in 5 s: a latency problem, not a failure
+        // no answer in 5 s (a latency problem, not a failure): retire the
+        // kernels and give the line up only once this one has left
+        (void)service_retire_locked(sv, nullptr);
+        r.quarantine = true;
         return kFallback;
     }
     if (q != hipSuccess) {
-        (void)service_reset_locked(sv);
+        (void)service_retire_locked(sv, nullptr);
+        r.quarantine = true;
         return hip_fail(q, "service stream");
     }
     // That kernel has left and this request is not fully answered (its
@@ -914,11 +974,13 @@ int service_progress(ServiceReq& r) {
     }
     // (a restart with fewer lines serves no workgroup on this one)
     if (sv.device < 0 || r.k >= sv.lines || ++r.relaunched > 3) return kFallback;
-    if (r.gen == sv.gen.load(std::memory_order_relaxed) || !service_waiting(sv, r.k, now))
+    if (r.gen == sv.gen.load(std::memory_order_relaxed) || !service_waiting(sv, r.k, now)) {
         if (int rc = service_launch_locked(sv)) {
-            (void)service_reset_locked(sv);
+            (void)service_retire_locked(sv, nullptr);  // this request's own kernel has left: no quarantine
             return rc;
         }
+        r.path |= PCS_PATH_NEW_GENERATION;
+    }
     // Re-arm the whole request: verdicts the old generation left must not
     // count as answers of the new one, whose workgroups re-hash those pages
     // (and would otherwise still be doing so once the host had released the
@@ -928,6 +990,7 @@ int service_progress(ServiceReq& r) {
     for (uint64_t i = 0; i < r.n; ++i) ok[i] = pcs::kServicePending;
     r.landed = 0;
     g_reposts.fetch_add(1, std::memory_order_relaxed);
+    r.path |= PCS_PATH_REPOSTED;
     r.gen = sv.gen.load(std::memory_order_relaxed);
     r.seq = service_post_locked(sv, r.k, r.gen);
     r.posted = Service::clock::now();
@@ -938,10 +1001,8 @@ int service_progress(ServiceReq& r) {
 int service_collect(ServiceReq& r, uint8_t* ok, uint64_t* first_bad) {
     Service& sv = *r.sv;
     const pcs::ServiceLine* ln = &sv.h->line[r.k];
-    {
-        std::lock_guard<std::mutex> lk(sv.mu);
-        sv.line[r.k].answered = Service::clock::now();
-    }
+    sv.line[r.k].answered.store(Service::clock::now().time_since_epoch().count(), std::memory_order_relaxed);
+    r.path |= PCS_PATH_SERVED;
     if (__atomic_load_n(&ln->torn_seq, __ATOMIC_RELAXED) == r.seq)
         g_torn_requests.fetch_add(1, std::memory_order_relaxed);
     if (!r.stamp) {
@@ -961,6 +1022,8 @@ int service_collect(ServiceReq& r, uint8_t* ok, uint64_t* first_bad) {
 
 // A synchronous host validate (ok != null) or stamp (ok == null) batch
 // through the service: PCS_OK, kNotServed (take the launch path) or < 0.
+thread_local int t_path = 0;  // pcs_last_path
+
 int service_run(Service* svp, const void* const* pages, uint64_t P, uint64_t n, int algo, uint8_t* ok,
                 uint64_t* first_bad) {
     ServiceReq r;
@@ -969,6 +1032,8 @@ int service_run(Service* svp, const void* const* pages, uint64_t P, uint64_t n, 
     int p;
     while ((p = service_progress(r)) == 0) __builtin_ia32_pause();  // the sibling hyperthread may be a shard thread
     int rc = p == 1 ? service_collect(r, ok, first_bad) : p == kFallback ? kNotServed : p;
+    if (p == kFallback) r.path |= PCS_PATH_FALLBACK;
+    t_path = r.path;
     service_release(r);
     return rc;
 }
@@ -1038,6 +1103,7 @@ struct pcs_batch {
     std::vector<const void*> svc_pages;
     std::vector<uint8_t> svc_ok;
     std::vector<uint64_t> svc_dig;
+    int path = 0;                      // PCS_PATH_* bits of the last submission (pcs_batch_path)
 };
 
 namespace {
@@ -1111,6 +1177,7 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
         b->cap_n = n;
     }
     b->zero_copy = false;
+    b->path |= PCS_PATH_LAUNCHED;
     b->stamp_pages.assign(n, nullptr);
     if (mode == PCS_BATCH_STAMP)
         for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
@@ -1156,6 +1223,7 @@ constexpr uint32_t kZcEventQueryPolls = 256;
 // was moved to the launch path), < 0 failed.
 int batch_service_poll(pcs_batch* b) {
     const int p = service_progress(b->svc);
+    b->path |= b->svc.path;
     if (p == 0) return 0;
     if (p == 1) {
         uint64_t fb = UINT64_MAX;
@@ -1178,6 +1246,7 @@ int batch_service_poll(pcs_batch* b) {
     b->via_service = false;
     if (p < 0) return batch_failed(b, p);
     // kFallback: the same pages on the launch path
+    b->path |= PCS_PATH_FALLBACK;
     if (int rc = batch_launch(b, b->mode, b->svc_pages.data(), b->P, b->n, b->algo)) return batch_failed(b, rc);
     return 0;
 }
@@ -1264,13 +1333,14 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
         return PCS_OK;
     }
     if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
+    t_path = 0;
     if (g_services_on.load(std::memory_order_relaxed) > 0) {
         if (int rc = check_host_batch_args(pages, page_size, n_pages, algo)) return rc;
         CallerGuard g(current_service(), page_size, n_pages, algo);
         const int r = service_run(g.service(), pages, page_size, n_pages, algo, ok, first_bad);
         if (r != kNotServed) return r;
-        return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
     }
+    t_path |= PCS_PATH_LAUNCHED;
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
 }
 
@@ -1294,10 +1364,21 @@ int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us) {
     if (e != hipSuccess) return hip_fail(e, "service start");
     // The stream is recreated (PCS_TUNE_SERVICE_STREAM is read here) unless
     // an asynchronous request of the previous run still owns a line and may
-    // be waiting on its kernel; the mailbox and the events are made once.
+    // be waiting on its kernel, a line is quarantined behind one, or the
+    // previous run's kernels have not left yet (a stop waits for them outside
+    // the lock; destroying the stream here would wait under it); the mailbox
+    // and the events are made once.
     bool owned = false;
-    for (auto& l : sv.line) owned |= l.owner.load(std::memory_order_acquire) != 0;
-    if (sv.stream && !owned) {
+    for (int k = 0; k < pcs::kServiceMaxLines; ++k) {
+        Service::Line& l = sv.line[k];
+        int q = 2;
+        if (l.owner.load(std::memory_order_acquire) == 2 && line_fence_passed(sv, k))
+            l.owner.compare_exchange_strong(q, 0, std::memory_order_acq_rel);
+        owned |= l.owner.load(std::memory_order_acquire) != 0;
+    }
+    const hipEvent_t last = sv.done[sv.gen.load(std::memory_order_relaxed) % kServiceEvents];
+    const bool left = !last || hipEventQuery(last) == hipSuccess;
+    if (sv.stream && !owned && left) {
         (void)hipStreamDestroy(sv.stream);
         sv.stream = nullptr;
     }
@@ -1342,27 +1423,27 @@ int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us) {
 int pcs_service_stop(void) {
     Service* svp = current_service();
     if (!svp) return PCS_OK;
-    std::lock_guard<std::mutex> lk(svp->mu);
-    return service_stop_locked(*svp);
+    return service_stop(*svp);
 }
 
 int pcs_service_running(void) {
     Service* svp = current_service();
-    if (!svp) return 0;
-    std::lock_guard<std::mutex> lk(svp->mu);
-    return svp->device >= 0 ? 1 : 0;
+    return svp && svp->device.load(std::memory_order_acquire) >= 0 ? 1 : 0;
 }
+
+int pcs_last_path(void) { return t_path; }
 
 int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_pages, int algo) {
     const void* const* cp = const_cast<const void* const*>(pages);
     if (injected_failure()) return fail(PCS_ERR_HIP, "injected failure (PCS_TUNE_FAIL_INJECT)");
+    t_path = 0;
     if (g_services_on.load(std::memory_order_relaxed) > 0) {
         if (int rc = check_host_batch_args(cp, page_size, n_pages, algo)) return rc;
         CallerGuard g(current_service(), page_size, n_pages, algo);
         const int r = service_run(g.service(), cp, page_size, n_pages, algo, nullptr, nullptr);
         if (r != kNotServed) return r;
-        return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);
     }
+    t_path |= PCS_PATH_LAUNCHED;
     return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);
 }
 
@@ -1451,6 +1532,7 @@ int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64
     b->first_bad = UINT64_MAX;
     b->all_ok = false;
     b->svc_results = false;
+    b->path = 0;
     if (mode < 0 || mode > 2) return fail(PCS_ERR_INVALID, "bad batch mode");
     if (int rc = check_flags(flags)) return rc;
     if ((flags & PCS_FLAG_SKIP_VERIFY) && mode != PCS_BATCH_VALIDATE)
@@ -1480,6 +1562,7 @@ int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64
             caller_enter(*svp);
             const int r = service_submit(b->svc, svp, pages, P, n, algo, mode == PCS_BATCH_STAMP);
             if (r == PCS_OK) {
+                b->path |= b->svc.path;
                 b->svc_pages.assign(pages, pages + n);
                 b->via_service = true;
                 b->state = 1;
@@ -1560,6 +1643,8 @@ int pcs_batch_result(pcs_batch* b, uint8_t* ok, uint64_t* digests, uint64_t* fir
     if (first_bad) *first_bad = b->first_bad;
     return PCS_OK;
 }
+
+int pcs_batch_path(const pcs_batch* b) { return b ? b->path : 0; }
 
 int pcs_batch_destroy(pcs_batch* b) {
     if (!b) return PCS_OK;

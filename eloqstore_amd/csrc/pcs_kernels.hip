@@ -1416,7 +1416,7 @@ uint64_t next_call_id() {
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 33;
+constexpr int kTuneKeys = 34;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1433,7 +1433,7 @@ constexpr int kTuneKeys = 33;
 // fails.
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
-                                      false, true,  false, false, false, true,  false, false, true};
+                                      false, true,  false, false, false, true,  false, false, true,  false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4/5 -> 1/2/4/3)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1457,7 +1457,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired (round 4 lab: XXH64 equal-byte runs)*/ 0,
                                           /*test only: service requests left to post as a stale partial answer*/ 0,
                                           /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 256,
-                                          /*retired (round 5 lab: service polls in flight)*/ 0};
+                                          /*retired (round 5 lab: service polls in flight)*/ 0,
+                                          /*test only: service kernels serve nothing and leave this many us late*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1908,8 +1909,12 @@ hipError_t run_flip(uint8_t* pages, uint64_t P, uint64_t n, uint64_t every, uint
 // +0.7 / +2.8 us per request (round 5, profiles/r05/service_poll_lab_r05k.txt):
 // the acquire that follows a served poll waits for the newer polls still in
 // flight, one more PCIe round trip on every request.
+//
+// exit_ticks (test only, PCS_TUNE_SERVICE_SLOW_EXIT_TEST): nonzero makes the
+// kernel a slow leaver for the non-blocking-poll test: it serves no request
+// and, once it has decided to leave, stays that many ticks longer.
 __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint64_t gen, uint64_t idle_ticks,
-                                                 uint64_t life_ticks) {
+                                                 uint64_t life_ticks, uint64_t exit_ticks) {
     constexpr int W = kServiceLineWords;
     __shared__ uint64_t s_line[W];
     __shared__ int s_go;
@@ -1930,7 +1935,7 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
                 const uint64_t w0 = __shfl(w, 0, 32);
                 // stop, or a newer generation queued behind this kernel
                 if (__shfl(w, W, 32) != 0 || __shfl(w, W + 1, 32) != gen) break;
-                if (w0 != last && (w0 >> 32) == gen) {
+                if (w0 != last && (w0 >> 32) == gen && exit_ticks == 0) {
                     uint64_t m = threadIdx.x == kServiceCheckWord || threadIdx.x >= W ? 0 : service_word_mix(w, threadIdx.x);
 #pragma unroll
                     for (int d = 1; d < W; d <<= 1) m += __shfl_xor(m, d, W);
@@ -1955,7 +1960,13 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
             if (threadIdx.x == 0) s_go = go;
         }
         __syncthreads();
-        if (!s_go) return;  // uniform per workgroup: idle, lifetime, stop or a newer generation
+        if (!s_go) {  // uniform per workgroup: idle, lifetime, stop or a newer generation
+            if (exit_ticks) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (__builtin_amdgcn_s_memrealtime() - t0 < exit_ticks) __builtin_amdgcn_s_sleep(127);
+            }
+            return;
+        }
         last = s_line[0];
         const uint64_t n = s_line[1];
         const uint32_t P = (uint32_t)s_line[2];
@@ -1985,10 +1996,10 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
 }
 
 hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                       hipStream_t s) {
+                       uint64_t exit_ticks, hipStream_t s) {
     if (lines < 1 || lines > kServiceMaxLines || wpl < 1 || lines * wpl > 256) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_service, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, (uint64_t)gen,
-                       idle_ticks, life_ticks);
+                       idle_ticks, life_ticks, exit_ticks);
     return hipGetLastError();
 }
 

@@ -163,6 +163,8 @@ public:
     // the batch size if every page matched.
     size_t FirstBad() const { return first_bad_; }
     const uint8_t* Verdicts() const { return ok_.data(); }
+    // PCS_PATH_* bits of the last submission: which path served it (pcs_batch_path).
+    int Path() const;
 
 private:
     int Collect();

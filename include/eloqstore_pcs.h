@@ -90,8 +90,10 @@ enum pcs_flags {
  *      PCS_COUNTER_SERVICE_TORN_REQUESTS; the C++ single-page SetChecksum /
  *      ValidateChecksum moved to libeloqstore_pcs_dropin.so
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
- *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed) */
-#define PCS_ABI_VERSION 5
+ *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
+ *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
+ *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST (additive) */
+#define PCS_ABI_VERSION 6
 int pcs_abi_version(void);
 const char *pcs_version(void);
 const char *pcs_last_error(void);
@@ -199,12 +201,31 @@ int pcs_batch_submit(pcs_batch *b, int mode, const void *const *pages, uint64_t 
  * submit with every verdict 1, sizing and pinning no staging. */
 int pcs_batch_submit_ex(pcs_batch *b, int mode, const void *const *pages, uint64_t page_size,
                         uint64_t n_pages, int algo, uint32_t flags);
-int pcs_batch_poll(pcs_batch *b);   /* 1 = done, 0 = in flight, < 0 = error */
+/* 1 = done, 0 = in flight, < 0 = error.  Never waits: on the service path a
+ * poll that finds the service's lock held (another thread starting, stopping
+ * or launching it) returns 0 and looks again at the next poll, and a service
+ * stop or restart never drains the stream under that lock. */
+int pcs_batch_poll(pcs_batch *b);
 int pcs_batch_wait(pcs_batch *b);   /* blocks until done; PCS_OK or error */
 /* After completion: verdicts / digests (either may be NULL) and the first
  * failing index (UINT64_MAX if none, validate mode). */
 int pcs_batch_result(pcs_batch *b, uint8_t *ok, uint64_t *digests, uint64_t *first_bad);
 int pcs_batch_destroy(pcs_batch *b);
+
+/* ---- which path served a host batch (diagnostics) ------------------------
+ * PCS_PATH_* bits of the calling thread's last synchronous host validate or
+ * stamp (pcs_pages_validate_host(_ex), pcs_pages_stamp_host), or of a batch's
+ * last submission (pcs_batch_path, complete or not).  0 before any call. */
+enum pcs_path {
+    PCS_PATH_SERVED = 1,          /* answered by the resident service kernel */
+    PCS_PATH_LAUNCHED = 2,        /* ran on the launch path (a kernel launch of its own) */
+    PCS_PATH_FALLBACK = 4,        /* posted to the service, then re-run on the launch path */
+    PCS_PATH_REPOSTED = 8,        /* re-posted to a newer service generation at least once */
+    PCS_PATH_NEW_GENERATION = 16, /* queued a new service kernel: none was certainly waiting */
+    PCS_PATH_LOCK_SKIPPED = 32,   /* a poll found the service's lock held and returned without it */
+};
+int pcs_last_path(void);
+int pcs_batch_path(const pcs_batch *b);
 
 /* ---- pre-armed validate service (small read batches, opt-in) --------------
  * A launch per host batch costs ~14 µs before its first page is read.  While
@@ -235,6 +256,10 @@ int pcs_service_start(int workgroups, uint32_t idle_us);
  * to `lines` calls on the device are in flight through the service at once,
  * each on a line of its own.  pcs_service_start(wg, idle) = _ex(1, wg, idle). */
 int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us);
+/* Turns the device's service off at once (new calls take the launch path),
+ * then waits, without holding anything another thread's call needs, up to 2 s
+ * for its kernels to leave; PCS_ERR_HIP if they have not.  Requests still in
+ * flight re-run on the launch path. */
 int pcs_service_stop(void);
 int pcs_service_running(void); /* 1 while the service is on, 0 otherwise */
 
@@ -330,6 +355,11 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     stale answer (validate 0, stamp 1); the
  *                                     host must re-arm and re-post the whole
  *                                     request (PCS_COUNTER_SERVICE_REPOSTS)
+ *   PCS_TUNE_SERVICE_SLOW_EXIT_TEST [0] test only: service kernels queued while
+ *                                     this is > 0 serve no request and stay
+ *                                     this many microseconds after deciding to
+ *                                     leave (a stop or restart must not make
+ *                                     pollers wait for them)
  * Keys 4, 5, 10, 12, 14, 16-22, 25, 29 and 32 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -357,6 +387,7 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_MAX_CALLERS = 28,
     PCS_TUNE_SERVICE_REPOST_TEST = 30,
     PCS_TUNE_ZC_STAMP_POLL_PAGES = 31,
+    PCS_TUNE_SERVICE_SLOW_EXIT_TEST = 33,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -19,6 +19,17 @@
 //      the gate off, four threads served on most calls with it on.
 // The CPU oracle is the checker.  Prints "service threads ok" on success.
 //
+// --slow-stop runs only the non-blocking-poll check: the
+// service's kernel serves nothing and leaves 300 ms after it is told to
+// (PCS_TUNE_SERVICE_SLOW_EXIT_TEST); an async batch is posted to it, another
+// thread calls pcs_service_stop, and this thread keeps polling the batch.
+// Every poll must return within 100 us while the stop waits for the kernel
+// (round 5 held the service's lock through a 2 s drain, so polls waited for
+// the whole exit), and the batch must come back exact through the launch
+// path.  --slow-timeout: the same kernel is never stopped; the request gives
+// up after 5 s, its line is quarantined until the kernel has left (a request
+// meanwhile takes the launch path), then the line serves again.
+//
 // --soak SECONDS runs only the soak instead: eight threads mix sync
 // validates, async validates and stamps of their own pages (every validate
 // with a corrupted page, every stamp over a zeroed header) while a controller
@@ -27,9 +38,14 @@
 // drills, and re-post drills (PCS_TUNE_SERVICE_REPOST_TEST: the next 1-4
 // requests are posted as a stale partial answer of an earlier generation,
 // which the host must re-arm and re-post).  Every result must be exact on whichever path served it; prints
-// the path mix, restarts and latency percentiles, then "service soak ok".
+// the path mix, restarts and latency percentiles -- overall and per op x
+// path (pcs_last_path / pcs_batch_path) x whether a restart was in flight,
+// plus the slowest requests with their attribution -- then "service soak ok".
 #include <algorithm>
+#include <array>
 #include <atomic>
+#include <map>
+#include <string>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -138,6 +154,197 @@ int env_mask(const char* name, int dflt) {
     return v && *v ? std::atoi(v) : dflt;
 }
 
+struct Sample {
+    float us, at_s;  // latency; start, seconds into the soak
+    int op, path, n;
+    bool restart;    // a service stop .. start overlapped the request
+};
+
+const char* op_name(int op) {
+    static const char* k[] = {"sync_validate", "async_validate", "sync_stamp", "async_stamp"};
+    return k[op & 3];
+}
+
+// served / served_new_gen / served_reposted / fallback / launched
+std::string path_class(int path) {
+    if (path & PCS_PATH_FALLBACK) return "fallback";
+    if (path & PCS_PATH_SERVED) {
+        if (path & PCS_PATH_REPOSTED) return "served_reposted";
+        if (path & PCS_PATH_NEW_GENERATION) return "served_new_gen";
+        return "served";
+    }
+    return "launched";
+}
+
+std::string path_bits(int path) {
+    std::string s;
+    const std::pair<int, const char*> bits[] = {{PCS_PATH_SERVED, "served"},       {PCS_PATH_LAUNCHED, "launched"},
+                                                {PCS_PATH_FALLBACK, "fallback"},   {PCS_PATH_REPOSTED, "reposted"},
+                                                {PCS_PATH_NEW_GENERATION, "new_gen"},
+                                                {PCS_PATH_LOCK_SKIPPED, "lock_skipped"}};
+    for (auto& b : bits)
+        if (path & b.first) s += (s.empty() ? "" : "+") + std::string(b.second);
+    return s.empty() ? "none" : s;
+}
+
+// Per op x path class x restart-in-flight: count, p50, p99.9, max; then the
+// ten slowest requests with their attribution.
+void print_attribution(std::vector<Sample>& all) {
+    std::map<std::string, std::vector<float>> cell;
+    for (const Sample& x : all)
+        cell[std::string(op_name(x.op)) + " " + path_class(x.path) + (x.restart ? " restart" : "")].push_back(x.us);
+    std::printf("soak attribution (op path [restart]: count p50 p99.9 max us)\n");
+    for (auto& [k, v] : cell) {
+        std::sort(v.begin(), v.end());
+        auto q = [&](double f) { return v[std::min(v.size() - 1, (size_t)(f * v.size()))]; };
+        std::printf("  %-40s %9zu %8.1f %9.1f %9.1f\n", k.c_str(), v.size(), q(0.5), q(0.999), v.back());
+    }
+    std::sort(all.begin(), all.end(), [](const Sample& a, const Sample& b) { return a.us > b.us; });
+    std::printf("soak slowest requests:\n");
+    for (size_t i = 0; i < std::min<size_t>(10, all.size()); ++i)
+        std::printf("  %9.1f us  at %7.3f s  %-14s n %3d  path %s%s\n", all[i].us, all[i].at_s, op_name(all[i].op),
+                    all[i].n, path_bits(all[i].path).c_str(), all[i].restart ? "  (restart in flight)" : "");
+}
+
+// --slow-stop / --slow-timeout: see the header.  Polls `b` until done,
+// timing each call; returns {polls, max us, polls over 100 us, max us of the
+// poll that re-launched the batch (the one whose path gained FALLBACK)}.
+struct PollStats {
+    uint64_t polls = 0, over = 0;
+    double max_us = 0, fallback_us = 0;
+};
+PollStats poll_timed(pcs_batch* b, double limit_s) {
+    PollStats st;
+    const auto end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(limit_s));
+    for (;;) {
+        const int before = pcs_batch_path(b);
+        const auto t0 = Clock::now();
+        const int x = pcs_batch_poll(b);
+        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        CHECK(x >= 0);
+        ++st.polls;
+        if (!(before & PCS_PATH_FALLBACK) && (pcs_batch_path(b) & PCS_PATH_FALLBACK)) {
+            st.fallback_us = us;  // this poll re-ran the pages on the launch path (a kernel launch)
+        } else {
+            st.max_us = std::max(st.max_us, us);
+            st.over += us > 100.0;
+        }
+        if (x == 1) return st;
+        CHECK(Clock::now() < end);
+    }
+}
+
+// n pages of the pool from page `first`, page k corrupted; submit + return
+std::vector<const void*> bad_batch(char* pool, size_t first, size_t n, size_t k) {
+    std::vector<const void*> v;
+    for (size_t i = 0; i < n; ++i) v.push_back(pool + (first + i) * P);
+    static_cast<char*>(const_cast<void*>(v[k]))[777] ^= 0x20;
+    return v;
+}
+void check_result(pcs_batch* b, std::vector<const void*>& v, size_t k) {
+    std::vector<uint8_t> ok(v.size(), 9);
+    uint64_t fb = 0;
+    CHECK(pcs_batch_result(b, ok.data(), nullptr, &fb) == PCS_OK);
+    static_cast<char*>(const_cast<void*>(v[k]))[777] ^= 0x20;  // heal
+    CHECK(fb == k);
+    for (size_t i = 0; i < v.size(); ++i) CHECK(ok[i] == (i != k));
+}
+
+int slow_stop(char* pool) {
+    constexpr int64_t kExitUs = 300000;
+    pcs_batch* b = nullptr;
+    CHECK(pcs_batch_create(&b) == PCS_OK);
+    // warm the batch's launch-path buffers (service off)
+    auto v = bad_batch(pool, 100, 40, 13);
+    CHECK(pcs_batch_submit(b, PCS_BATCH_VALIDATE, v.data(), P, v.size(), PCS_XXH3_64) == PCS_OK);
+    CHECK(pcs_batch_wait(b) == PCS_OK);
+    check_result(b, v, 13);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 0) == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_SLOW_EXIT_TEST, kExitUs) == PCS_OK);
+    CHECK(pcs_service_start_ex(1, 1, 1000000) == PCS_OK);  // 1 s idle: the kernel stays until stopped
+    v = bad_batch(pool, 200, 40, 21);
+    CHECK(pcs_batch_submit(b, PCS_BATCH_VALIDATE, v.data(), P, v.size(), PCS_XXH3_64) == PCS_OK);
+    CHECK(pcs_batch_path(b) & PCS_PATH_NEW_GENERATION);  // posted to a kernel it queued
+    // 20 ms of polls: the kernel serves nothing
+    const auto t_hold = Clock::now() + std::chrono::milliseconds(20);
+    while (Clock::now() < t_hold) CHECK(pcs_batch_poll(b) == 0);
+    std::atomic<int> stop_rc{-100};
+    std::atomic<double> stop_ms{0};
+    std::thread stopper([&] {
+        const auto s0 = Clock::now();
+        stop_rc = pcs_service_stop();
+        stop_ms = std::chrono::duration<double, std::milli>(Clock::now() - s0).count();
+    });
+    const auto p0 = Clock::now();
+    const PollStats st = poll_timed(b, 10.0);
+    const double poll_ms = std::chrono::duration<double, std::milli>(Clock::now() - p0).count();
+    stopper.join();
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_SLOW_EXIT_TEST, 0) == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
+    const int path = pcs_batch_path(b);
+    std::printf("slow stop: pcs_service_stop rc %d in %.1f ms (kernel exit delay %lld ms); batch done after %.1f ms "
+                "of polls: %llu polls, max %.1f us, %llu over 100 us (the re-launching poll: %.1f us); path %s\n",
+                stop_rc.load(), stop_ms.load(), (long long)kExitUs / 1000, poll_ms, (unsigned long long)st.polls,
+                st.max_us, (unsigned long long)st.over, st.fallback_us, path_bits(path).c_str());
+    CHECK(stop_rc == PCS_OK);
+    CHECK(stop_ms >= 0.8 * kExitUs / 1000);  // the stop really waited for the slow kernel ...
+    CHECK(poll_ms >= 0.8 * kExitUs / 1000);  // ... and the batch was polled all that time
+    CHECK((path & PCS_PATH_FALLBACK) && (path & PCS_PATH_LAUNCHED) && !(path & PCS_PATH_SERVED));
+    check_result(b, v, 21);
+    CHECK(st.over == 0 && st.max_us < 100.0);
+    CHECK(st.fallback_us < 2000.0);
+    pcs_batch_destroy(b);
+    return 0;
+}
+
+int slow_timeout(char* pool) {
+    constexpr int64_t kExitUs = 5000000;  // idle 1 s + 5 s late: still there when the request gives up at 5 s
+    pcs_batch* b = nullptr;
+    CHECK(pcs_batch_create(&b) == PCS_OK);
+    auto v = bad_batch(pool, 100, 40, 5);
+    CHECK(pcs_batch_submit(b, PCS_BATCH_VALIDATE, v.data(), P, v.size(), PCS_XXH3_64) == PCS_OK);
+    CHECK(pcs_batch_wait(b) == PCS_OK);
+    check_result(b, v, 5);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 0) == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_SLOW_EXIT_TEST, kExitUs) == PCS_OK);
+    CHECK(pcs_service_start_ex(1, 1, 1000000) == PCS_OK);
+    v = bad_batch(pool, 300, 60, 44);
+    const auto p0 = Clock::now();
+    CHECK(pcs_batch_submit(b, PCS_BATCH_VALIDATE, v.data(), P, v.size(), PCS_XXH3_64) == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_SLOW_EXIT_TEST, 0) == PCS_OK);  // later kernels serve again
+    const PollStats st = poll_timed(b, 20.0);
+    const double gave_up_s = std::chrono::duration<double>(Clock::now() - p0).count();
+    const int path = pcs_batch_path(b);
+    check_result(b, v, 44);
+    CHECK((path & PCS_PATH_FALLBACK) && !(path & PCS_PATH_SERVED) && !(path & PCS_PATH_REPOSTED));
+    CHECK(gave_up_s >= 4.9 && gave_up_s < 6.0);
+    CHECK(st.over == 0 && st.max_us < 100.0);
+    // the line is quarantined until the slow kernel has left (~6 s after the
+    // submit): a request now takes the launch path ...
+    v = bad_batch(pool, 500, 8, 2);
+    CHECK(pcs_batch_submit(b, PCS_BATCH_VALIDATE, v.data(), P, v.size(), PCS_XXH3_64) == PCS_OK);
+    CHECK(pcs_batch_wait(b) == PCS_OK);
+    const int q_path = pcs_batch_path(b);
+    check_result(b, v, 2);
+    CHECK(q_path == PCS_PATH_LAUNCHED);
+    // ... and once it has, the line serves again
+    while (Clock::now() - p0 < std::chrono::milliseconds(6600)) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    v = bad_batch(pool, 600, 8, 7);
+    CHECK(pcs_batch_submit(b, PCS_BATCH_VALIDATE, v.data(), P, v.size(), PCS_XXH3_64) == PCS_OK);
+    CHECK(pcs_batch_wait(b) == PCS_OK);
+    const int s_path = pcs_batch_path(b);
+    check_result(b, v, 7);
+    std::printf("slow timeout: request gave up after %.2f s (%llu polls, max %.1f us, %llu over 100 us, re-launching "
+                "poll %.1f us), path %s; while quarantined: %s; after the kernel left: %s\n",
+                gave_up_s, (unsigned long long)st.polls, st.max_us, (unsigned long long)st.over, st.fallback_us,
+                path_bits(path).c_str(), path_bits(q_path).c_str(), path_bits(s_path).c_str());
+    CHECK(s_path & PCS_PATH_SERVED);
+    CHECK(pcs_service_stop() == PCS_OK);
+    CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
+    pcs_batch_destroy(b);
+    return 0;
+}
+
 int soak(char* pool, int T, double secs) {
     const int ops = env_mask("PCS_SOAK_OPS", 15), ctl = env_mask("PCS_SOAK_CTL", 15);
     std::vector<int> op_list;
@@ -148,6 +355,11 @@ int soak(char* pool, int T, double secs) {
     std::atomic<bool> done{false};
     std::atomic<uint64_t> n_sync{0}, n_async{0}, n_stamp{0};
     std::vector<std::vector<float>> lat(T);
+    // attribution: every request's op, path bits, size, whether a service
+    // restart (stop .. start) overlapped it, and when it started
+    std::vector<std::vector<Sample>> smp(T);
+    std::atomic<uint64_t> restart_epoch{0};  // odd while the controller is between stop and start
+    const auto soak_t0 = Clock::now();
     const Counts c0 = counts();
     const uint64_t torn0 = pcs_counter(PCS_COUNTER_SERVICE_TORN_REQUESTS);
     const uint64_t reposts0 = pcs_counter(PCS_COUNTER_SERVICE_REPOSTS);
@@ -171,8 +383,10 @@ int soak(char* pool, int T, double secs) {
             while (!done.load(std::memory_order_relaxed)) {
                 const int op = op_list[splitmix(rng) % op_list.size()];
                 Req r = make_req(pool, t, rng, splitmix(rng) % 4 ? 24 : 256);
+                const uint64_t ep0 = restart_epoch.load(std::memory_order_acquire);
                 const auto t0 = Clock::now();
                 bool good = true;
+                int path = 0;
                 if (op >= 2) {  // stamp over zeroed headers (op 3: async, digests checked too)
                     std::vector<char*> w;
                     for (const char* p : r.ptrs) {
@@ -182,6 +396,7 @@ int soak(char* pool, int T, double secs) {
                     const Counts s0 = counts();
                     if (op == 2) {
                         eloqstore::SetChecksums(w, P);
+                        path = pcs_last_path();
                     } else {
                         CHECK(pcs_batch_submit(sb, PCS_BATCH_STAMP, reinterpret_cast<const void* const*>(w.data()), P,
                                                w.size(), PCS_XXH3_64) == PCS_OK);
@@ -189,6 +404,7 @@ int soak(char* pool, int T, double secs) {
                         while ((x = pcs_batch_poll(sb)) == 0) {
                         }
                         CHECK(x == 1);
+                        path = pcs_batch_path(sb);
                         dig.assign(w.size(), 0);
                         CHECK(pcs_batch_result(sb, nullptr, dig.data(), nullptr) == PCS_OK);
                         for (size_t i = 0; i < w.size(); ++i)
@@ -235,18 +451,25 @@ int soak(char* pool, int T, double secs) {
                         }
                         fb = cb.FirstBad();
                         v = cb.Verdicts();
+                        path = cb.Path();
                         n_async.fetch_add(1, std::memory_order_relaxed);
                     } else {
                         ok.assign(r.ptrs.size(), 9);
                         fb = eloqstore::ValidateChecksums(r.ptrs, P, ok.data());
                         v = ok.data();
+                        path = pcs_last_path();
                         n_sync.fetch_add(1, std::memory_order_relaxed);
                     }
                     bad[r.byte] ^= 0x04;
                     good = fb == r.k;
                     for (size_t i = 0; i < r.ptrs.size(); ++i) good &= v[i] == (i != r.k);
                 }
-                lat[t].push_back(std::chrono::duration<float, std::micro>(Clock::now() - t0).count());
+                const auto t1 = Clock::now();
+                const uint64_t ep1 = restart_epoch.load(std::memory_order_acquire);
+                const float us = std::chrono::duration<float, std::micro>(t1 - t0).count();
+                lat[t].push_back(us);
+                smp[t].push_back({us, (float)std::chrono::duration<double>(t0 - soak_t0).count(), op, path,
+                                  (int)r.ptrs.size(), ep0 != ep1 || (ep0 & 1)});
                 if (!good && errors.fetch_add(1) < 5)
                     std::fprintf(stderr, "soak thread %d: op %d n %zu slot %zu wrong\n", t, op, r.ptrs.size(), r.k);
             }
@@ -262,6 +485,7 @@ int soak(char* pool, int T, double secs) {
         if (!(ctl & (action == 0 ? 1 : action <= 2 ? 2 : action == 3 ? 4 : 8))) continue;
         switch (action) {
         case 0: {  // restart with another shape
+            restart_epoch.fetch_add(1, std::memory_order_acq_rel);
             CHECK(pcs_service_stop() == PCS_OK);
             if (splitmix(rng) % 3 == 0) {  // a stretch with no service at all
                 const int ms = 1 + (int)(splitmix(rng) % 10);
@@ -271,6 +495,7 @@ int soak(char* pool, int T, double secs) {
             const int lines = 1 << (splitmix(rng) % 4), wpl = 1 << (splitmix(rng) % 3);
             const uint32_t idles[] = {0, 200, 500, 5000};
             CHECK(pcs_service_start_ex(lines, wpl, idles[splitmix(rng) % 4]) == PCS_OK);
+            restart_epoch.fetch_add(1, std::memory_order_acq_rel);
             ++restarts;
             break;
         }
@@ -314,6 +539,9 @@ int soak(char* pool, int T, double secs) {
                 (unsigned long long)(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) - reposts0));
     std::printf("soak latency us: p50 %.1f  p99 %.1f  p99.9 %.1f  max %.1f\n", pct(0.5), pct(0.99), pct(0.999),
                 all.empty() ? 0.f : all.back());
+    std::vector<Sample> every;
+    for (auto& v : smp) every.insert(every.end(), v.begin(), v.end());
+    print_attribution(every);
     CHECK((c1.served > c0.served || !service_on) && (ctl != 15 || (c1.launched > c0.launched && restarts > 0)));
     return errors.load();
 }
@@ -327,6 +555,13 @@ int main(int argc, char** argv) {
     oracle_fill_pages(pool, P, np, 0x7E57, 0);
     for (size_t i = 0; i < np; ++i) oracle_set_checksum(pool + i * P, P);
     eloqstore::RegisterPagePool(pool, np * P);
+    if (argc == 2 && (std::strcmp(argv[1], "--slow-stop") == 0 || std::strcmp(argv[1], "--slow-timeout") == 0)) {
+        CHECK((std::strcmp(argv[1], "--slow-stop") == 0 ? slow_stop(pool) : slow_timeout(pool)) == 0);
+        eloqstore::UnregisterPagePool(pool);
+        std::free(pool);
+        std::printf("%s ok\n", argv[1] + 2);
+        return 0;
+    }
     if (argc == 3 && std::strcmp(argv[1], "--soak") == 0) {
         CHECK(soak(pool, T, std::atof(argv[2])) == 0);
         eloqstore::UnregisterPagePool(pool);

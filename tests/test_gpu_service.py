@@ -758,3 +758,27 @@ def test_service_toggled_under_threads(no_gate):
         assert not errors, errors[:5]
         assert min(calls) > 20 and pcs.counter(SVC) > s0
         assert pcs.lib().pcs_service_running() == 0
+
+
+@pytest.mark.parametrize("mode", ["--slow-stop", "--slow-timeout"])
+def test_poll_never_waits_on_a_slow_service_exit(mode):
+    """ChecksumBatch::Poll / pcs_batch_poll must never block
+    (shard.cpp:118-125: one poll that blocks stalls every coroutine of the
+    shard).  tests/cpp/service_threads_test.cpp with the service kernel made
+    a slow leaver (PCS_TUNE_SERVICE_SLOW_EXIT_TEST: it serves nothing and
+    stays after it is told to leave).
+    --slow-stop: another thread's pcs_service_stop waits ~300 ms for the
+    kernel while this thread polls an async batch posted to it: every poll
+    returns within 100 us (round 5 held the service's lock through the
+    drain), the stop really took the 300 ms, and the batch comes back exact
+    through the launch path.
+    --slow-timeout: nobody stops it; the request gives up after 5 s (polls
+    still under 100 us), re-runs exact on the launch path, and its line is
+    quarantined until the kernel has left: a request meanwhile is launched,
+    and the line serves again afterwards."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "service_threads_test")
+    r = subprocess.run([exe, mode], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and f"{mode[2:]} ok" in r.stdout, r.stdout + r.stderr
+    print(r.stdout)
