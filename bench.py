@@ -231,24 +231,50 @@ class Workload:
         # 8 B digest (digest), 1 B verdict (validate), 8 B into the page (stamp)
         return self.bytes + (1 if mode == "validate" else 8) * self.n
 
-    def stream_read(self, reps: int) -> float | None:
-        """GB/s of the batch buffer read by the plain streaming-read kernel
-        (no hash): pcs_stream_read_dev over the whole buffer."""
-        scratch = torch.empty((self.bytes + 65535) // 65536, dtype=torch.int64, device=self.dev)
+    def ceiling_ab(self, rounds: int = 7, per: int = 20, settle_ms: float = 200.0):
+        """The streaming-read ceiling (SURVEY §8d) against the hash kernel
+        under ONE protocol: pcs_stream_read_dev (k_stream_read: the headline
+        kernel's structure and loads, no hash) and the digest step alternate
+        in `rounds` rounds of `per` launches each, every round bracketed by
+        HIP events on the launch stream, after `settle_ms` of both; medians.
+        Both move the same bytes (every page byte read, 8 B per 4 KiB page
+        written), so their GB/s are directly comparable and frac_of_ceiling
+        = hash / ceiling.  Round 5 timed the reader alone for 3 launches
+        right after host-side work (the part idling), so it read ~4 % below
+        the hash kernel it was meant to bound (VERDICT r05 #6)."""
+        import statistics
+        scratch = torch.empty((self.bytes + 4095) // 4096, dtype=torch.int64, device=self.dev)
 
-        def run():
+        def read():
             pcs.stream_read(self.pages, self.bytes, scratch)
 
-        run()
-        torch.cuda.synchronize()
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        for _ in range(reps):
-            run()
-        ev[1].record()
-        torch.cuda.synchronize()
-        t = ev[0].elapsed_time(ev[1]) / 1e3 / reps
-        return self.bytes / t / 1e9
+        def hash_():
+            self.step("digest")
+
+        t_end = time.perf_counter() + settle_ms / 1e3
+        while time.perf_counter() < t_end:
+            for _ in range(4):
+                read()
+                hash_()
+            torch.cuda.synchronize()
+        times = {"read": [], "hash": []}
+        for r in range(rounds):
+            order = (("read", read), ("hash", hash_)) if r % 2 == 0 else (("hash", hash_), ("read", read))
+            for name, fn in order:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                for _ in range(per):
+                    fn()
+                ev1.record()
+                torch.cuda.synchronize()
+                times[name].append(ev0.elapsed_time(ev1) / 1e3 / per)
+        moved = self.bytes + 8 * ((self.bytes + 4095) // 4096)
+        read_gbps = moved / statistics.median(times["read"]) / 1e9
+        hash_gbps = self.algorithmic_bytes("digest") / statistics.median(times["hash"]) / 1e9
+        return {"stream_read_GBps": round(read_gbps, 1), "hash_GBps": round(hash_gbps, 1),
+                "frac_of_ceiling": round(hash_gbps / read_gbps, 4),
+                "protocol": f"{rounds} alternating rounds of {per} launches each (HIP events per round), "
+                            f"after {settle_ms:.0f} ms of both; medians; the same bytes moved by both"}
 
     def sample_pages_host(self, max_bytes: int):
         """(host uint8 array, page size, gpu digests) for a leading sample of the batch."""
@@ -530,10 +556,25 @@ def config1(target_s: float, all_cores_s: float | None, workdir: str | None = No
         shutil.rmtree(d, ignore_errors=True)
 
 
+PCIE_GEN5_X16_GBPS = 63.0  # PCIe Gen5 x16 per direction, after 128b/130b encoding (≈ 63 GB/s)
+
+
 def host_inclusive(w: Workload, max_pages: int = 1 << 18):
-    """Pages starting in host memory: H2D + kernel + D2H of digests, through
-    pcs_pages_digest_host.  (a) one contiguous pinned run -> direct DMA;
-    (b) pageable pages -> gather into pinned staging.  Not the headline value."""
+    """Pages starting in host memory (SURVEY §8d "host-inclusive"; north_star:
+    "the rate including pinned hipMemcpyAsync to and from the GPU"), 1 GiB of
+    the headline's pages, each leg through pcs_pages_digest_host:
+      direct_pinned        one contiguous pinned run: pinned hipMemcpyAsync
+                           H2D -> kernel -> D2H of the digests (32 MiB chunks
+                           over three streams)
+      gather_pageable      pageable pages gathered into pinned staging first
+      gather_scattered     pool pages in random order, unregistered: gather
+      zero_copy_scattered  the same pages in a registered pool: one launch
+                           reading them in place over PCIe (the reference
+                           consumer's shape: ReadPages validating host pool
+                           pages, async_io_manager.cpp:353-366)
+    Each leg's digests are compared with the device-resident run's
+    (parity: mismatches), and its rate is given as a fraction of PCIe Gen5
+    x16 (63 GB/s).  Not the headline value."""
     if w.P is None:
         return None
     k = min(w.n, max_pages)
@@ -542,39 +583,42 @@ def host_inclusive(w: Workload, max_pages: int = 1 << 18):
     pinned.copy_(w.pages[:nbytes])
     pageable = pinned.numpy().copy()
     digests = np.empty(k, dtype=np.uint64)
-    res = {"pages": k, "page_size": w.P, "bytes": nbytes}
-    for name, base in (("direct_pinned", pinned.data_ptr()), ("gather_pageable", pageable.ctypes.data)):
-        ptrs = (np.arange(k, dtype=np.uint64) * np.uint64(w.P) + np.uint64(base))
+    dev_digests = w.out[:k].cpu().numpy().view(np.uint64)
+    res = {"pages": k, "page_size": w.P, "bytes": nbytes, "pcie_peak_GBps": PCIE_GEN5_X16_GBPS, "legs": {}}
+
+    def leg(name, ptrs, want, how):
         fn = pcs.lib().pcs_pages_digest_host
         rc = fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)  # warm (allocates staging)
         assert rc == 0, pcs.lib().pcs_last_error()
         reps, t0 = 0, time.perf_counter()
         while reps < 3 or time.perf_counter() - t0 < 2.0:
-            fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)
-            reps += 1
-        dt = (time.perf_counter() - t0) / reps
-        res[f"{name}_GiBps"] = round(nbytes / dt / GIB, 2)
-        res[f"{name}_digests_match_device"] = bool(np.array_equal(digests, w.out[:k].cpu().numpy().view(np.uint64)))
-    # Scattered pool pages (a random permutation, like pages spread over
-    # PagesPool chunks): (c) unregistered -> gather; (d) registered pool ->
-    # zero-copy, one launch reading the pages in place.
-    perm = np.random.default_rng(7).permutation(k).astype(np.uint64)
-    want = w.out[:k].cpu().numpy().view(np.uint64)[perm]
-    with pcs.PagePool(k, w.P) as pool:
-        pool.pages.reshape(-1)[:] = pageable
-        for name, base in (("gather_scattered", pageable.ctypes.data), ("zero_copy_scattered", pool.base)):
-            ptrs = perm * np.uint64(w.P) + np.uint64(base)
-            fn = pcs.lib().pcs_pages_digest_host
             rc = fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)
             assert rc == 0, pcs.lib().pcs_last_error()
-            reps, t0 = 0, time.perf_counter()
-            while reps < 3 or time.perf_counter() - t0 < 2.0:
-                fn(ptrs.ctypes.data, w.P, k, w.algo, digests.ctypes.data)
-                reps += 1
-            dt = (time.perf_counter() - t0) / reps
-            res[f"{name}_GiBps"] = round(nbytes / dt / GIB, 2)
-            res[f"{name}_digests_match_device"] = bool(np.array_equal(digests, want))
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+        res["legs"][name] = {"GiBps": round(nbytes / dt / GIB, 2), "GBps": round(nbytes / dt / 1e9, 2),
+                             "frac_of_pcie": round(nbytes / dt / 1e9 / PCIE_GEN5_X16_GBPS, 4),
+                             "calls": reps, "parity_mismatches": int((digests != want).sum()), "how": how}
+        res[f"{name}_GiBps"] = res["legs"][name]["GiBps"]
+
+    for name, base, how in (("direct_pinned", pinned.data_ptr(),
+                             "pinned hipMemcpyAsync H2D -> XXH3 kernel -> D2H of digests"),
+                            ("gather_pageable", pageable.ctypes.data,
+                             "memcpy gather into pinned staging, then as direct_pinned")):
+        leg(name, np.arange(k, dtype=np.uint64) * np.uint64(w.P) + np.uint64(base), dev_digests, how)
+    # Scattered pool pages (a random permutation, like pages spread over
+    # PagesPool chunks): unregistered -> gather; registered pool -> zero-copy
+    perm = np.random.default_rng(7).permutation(k).astype(np.uint64)
+    want = dev_digests[perm]
+    with pcs.PagePool(k, w.P) as pool:
+        pool.pages.reshape(-1)[:] = pageable
+        for name, base, how in (("gather_scattered", pageable.ctypes.data,
+                                 "scattered pageable pages gathered into pinned staging"),
+                                ("zero_copy_scattered", pool.base,
+                                 "scattered pages of a registered pool read in place by one launch")):
+            leg(name, perm * np.uint64(w.P) + np.uint64(base), want, how)
         res["batch_latency_us"] = batch_latency(pool, pageable, w)
+    res["parity_mismatches"] = sum(v["parity_mismatches"] for v in res["legs"].values())
     return res
 
 
@@ -652,6 +696,32 @@ def settle(w: Workload, mode: str, ms: float) -> int:
         n += 8
         torch.cuda.synchronize()
     return n
+
+
+def cold_rate(dist, w: Workload, mode: str, steps: int, warmup: int) -> dict:
+    """The headline protocol without the settle: `warmup` steps, then
+    `steps` steps timed (host clock between barriers, HIP events on the
+    launch stream), at the start of the process."""
+    for _ in range(warmup):
+        w.step(mode)
+    torch.cuda.synchronize()
+    barrier(dist)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        w.step(mode)
+    ev1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t1 - t0)
+    value = sum_over_ranks(dist, float(w.bytes)) * steps / elapsed / GIB
+    avg = ev0.elapsed_time(ev1) / 1e3 / steps
+    return {"value": round(value, 2), "unit": "GiB/s", "steps": steps, "warmup": warmup,
+            "frac": round(w.algorithmic_bytes(mode) / avg / 1e9 / HBM_PEAK_GBPS, 4),
+            "avg_launch_ms": round(avg * 1e3, 4),
+            "protocol": "the driver's warmup + timed steps at process start, no settle (rank 0's kernel for frac)"}
 
 
 def timed_launches(w: Workload, mode: str, steps: int, warmup: int, rounds: int = 1) -> float:
@@ -778,49 +848,60 @@ MULTI_SWEEP = (("config7_xxh3", 7), ("config4_xxh3", 4))
 
 
 def multi_rank_sweep(dist, world: int, rank: int, dev: str, algo: int, steps: int, warmup: int, scale: int,
-                     settle_ms: float = SWEEP_SETTLE_MS):
+                     settle_ms: float = SWEEP_SETTLE_MS, deadline: float | None = None):
     """Each entry on every rank: its own shard of the config (global page
     indices rank * n ...), `steps` launches timed between barriers, value =
     bytes of all ranks / the max-over-ranks wall time, then parity and the
     drill on every rank.  Every rank reaches every collective: a local
-    failure is recorded, never raised."""
+    failure (build, settle, warmup, the timed launches, parity, drill) is
+    recorded, never raised, and the ranks agree on success (min over ranks)
+    before and after the timed section, so no rank waits on a rank that has
+    failed.  Entries past the wall deadline (on any rank) are skipped."""
     out = []
     for key, cfg in MULTI_SWEEP:
+        late = deadline is not None and time.perf_counter() > deadline
+        if min_over_ranks(dist, 0.0 if late else 1.0) < 1.0:
+            out.append({"key": key, "config": cfg, "skipped": "bench wall budget spent"})
+            continue
         w, err = None, None
         try:
             w = Workload(cfg, algo, rank, max(1, CONFIGS[cfg][1] // scale), dev)
+            settle(w, "digest", settle_ms)
+            for _ in range(warmup):
+                w.step("digest")
+            torch.cuda.synchronize()
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"[:300]
         if min_over_ranks(dist, 0.0 if err else 1.0) < 1.0:
-            out.append({"key": key, "config": cfg, "error": err or "another rank failed to build its shard"})
-            w = None
+            out.append({"key": key, "config": cfg, "error": err or "another rank failed to build or warm its shard"})
+            if w is not None:
+                w.free()
             continue
-        settle(w, "digest", settle_ms)
-        for _ in range(warmup):
-            w.step("digest")
-        torch.cuda.synchronize()
         barrier(dist)
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record()
-        for _ in range(steps):
-            w.step("digest")
-        ev1.record()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
+        t0 = t1 = time.perf_counter()
+        avg = None
+        try:
+            torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            ev0.record()
+            for _ in range(steps):
+                w.step("digest")
+            ev1.record()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            avg = ev0.elapsed_time(ev1) / 1e3 / steps
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"[:300]
         barrier(dist)
+        if min_over_ranks(dist, 0.0 if err else 1.0) < 1.0:
+            out.append({"key": key, "config": cfg, "error": err or "another rank failed in the timed section"})
+            w.free()
+            continue
         elapsed = max_over_ranks(dist, t1 - t0)
         total = sum_over_ranks(dist, float(w.bytes)) * steps
-        avg = ev0.elapsed_time(ev1) / 1e3 / steps
-        try:
-            par = parity_sample(w)
-        except Exception as e:  # noqa: BLE001
-            par = {"error": f"{type(e).__name__}: {e}"[:300]}
-        try:
-            drill = w.corruption_drill()
-        except Exception as e:  # noqa: BLE001
-            drill = {"error": f"{type(e).__name__}: {e}"[:300], "pass": False}
+        par = guarded_check(parity_sample, w)
+        drill = guarded_check(w.corruption_drill)
         checks, ok = gather_checks(dist, world, rank, par, drill)
         value = total / elapsed / GIB
         alg = w.algorithmic_bytes("digest")
@@ -934,6 +1015,17 @@ def live_traffic(timeout_s: int = 90):
                       "(read = FETCH_SIZE*1024*2, write = WRITE_SIZE*1024, median over dispatches)"}
 
 
+def guarded_check(fn, *a, **kw):
+    """A parity sample or drill that raises becomes a failing record
+    ({"error", "pass": False}) instead of an exception."""
+    try:
+        return fn(*a, **kw)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        return {"error": f"{type(e).__name__}: {e}"[:300], "pass": False}
+
+
 def guarded(name: str, fn, *a, **kw):
     """fn(*a, **kw), or {"error": ...} if it raises (the traceback goes to
     stderr): an optional leg never takes the headline line down with it."""
@@ -966,7 +1058,9 @@ def main():
     ap.add_argument("--sweep-scale", type=int, default=1,
                     help="divide every sweep workload's page count (tests only; default 1 = the BASELINE sizes)")
     ap.add_argument("--host-inclusive", action="store_true",
-                    help="also time the host-memory path (pinned direct DMA and pageable gather)")
+                    help="(default at N=1) time the host-memory paths too")
+    ap.add_argument("--no-host-inclusive", action="store_true",
+                    help="skip the host-memory legs (pinned H2D -> kernel -> D2H, gather, zero-copy)")
     ap.add_argument("--no-live-traffic", action="store_true",
                     help="take roofline.traffic from the committed profiles/ summary instead of two rocprofv3 "
                          "--pmc passes in this run")
@@ -1019,6 +1113,10 @@ def main():
     # process) and 0.15 % at 400 steps (tools/lab/bench_gap_lab.py,
     # profiles/r05/bench_gap_r05y.txt): the part slows down while idle, and the
     # warmup exists to bring it back before the clock starts.
+    time.sleep(PHASE_GAP_S)
+    # The driver's own protocol first, with no settle: W
+    # warmup steps, then K timed steps, on the part as the process finds it.
+    cold = cold_rate(dist, w, args.mode, min(args.steps, 400), args.warmup)
     time.sleep(PHASE_GAP_S)
     settle_steps = settle(w, args.mode, args.settle_ms)
     for _ in range(args.warmup):
@@ -1084,10 +1182,12 @@ def main():
     # Parity and the corruption drill on EVERY rank, each over its own shard
     # (SURVEY §8d "parity in every run", §8e partitioning); rank 0's line
     # carries them all and the run fails if any rank's does.
-    parity = parity_sample(w)
-    stream_rate = w.stream_read(max(3, args.steps // 20))
+    # Each guarded per rank: a rank whose check raises records
+    # it as failed and still reaches the gather, so no rank waits forever.
+    parity = guarded_check(parity_sample, w)
+    ceiling = guarded("ceiling", w.ceiling_ab) if args.mode == "digest" and w.P == 4096 else None
     time.sleep(PHASE_GAP_S)
-    drill = w.corruption_drill()
+    drill = guarded_check(w.corruption_drill)
     time.sleep(PHASE_GAP_S)
     per_rank_checks, checks_ok = gather_checks(dist, world, rank, parity, drill)
     # Optional legs, each guarded: a failure is recorded under its key and the
@@ -1098,14 +1198,14 @@ def main():
     # the wall budget are skipped, and config 1 is skipped when the time left
     # cannot hold it.
     hostinc = None
-    if args.host_inclusive and rank == 0:
+    if not args.no_host_inclusive and rank == 0 and world == 1:
         hostinc = guarded("host_inclusive", host_inclusive, w) if time.perf_counter() < deadline else \
             {"skipped": "bench wall budget spent"}
     multi_entries = None
     if world > 1 and not args.no_sweep:
         multi_entries = multi_rank_sweep(dist, world, rank, dev, algo, args.sweep_steps, args.sweep_warmup,
-                                         max(1, args.sweep_scale), min(args.settle_ms, SWEEP_SETTLE_MS))
-        checks_ok = checks_ok and all(e.get("checks_all_ranks_pass") for e in multi_entries)
+                                         max(1, args.sweep_scale), min(args.settle_ms, SWEEP_SETTLE_MS), deadline)
+        checks_ok = checks_ok and all(e.get("checks_all_ranks_pass") for e in multi_entries if "skipped" not in e)
     sweep_entries = None
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep_entries = guarded("sweep", sweep, dev, args.sweep_steps, args.sweep_warmup,
@@ -1165,6 +1265,9 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                # achieved / the measured streaming-read ceiling of the same bytes (ceiling_ab)
+                "frac_of_ceiling": round(achieved / ceiling["stream_read_GBps"], 4)
+                if ceiling and ceiling.get("stream_read_GBps") else None,
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
                 "traffic_live": live,
@@ -1172,7 +1275,9 @@ def main():
                 "avg_launch_ms": round(avg_launch * 1e3, 4),
                 "launch_timing": f"HIP events bracketing the {args.steps} timed steps on the launch stream",
             },
-            "stream_read_GBps": round(stream_rate, 1) if stream_rate else None,
+            "stream_read_GBps": ceiling.get("stream_read_GBps") if ceiling else None,
+            "ceiling": ceiling,
+            "cold": cold,
             "cpu_baseline": c1.get("cpu_baseline") if c1 else None,
             "parity": parity,
         }
@@ -1191,6 +1296,9 @@ def main():
         if scaling is not None:
             line["scaling_detail"] = scaling
         if hostinc is not None:
+            if c1 and c1.get("cpu_ref_inmem_all_cores") and not hostinc.get("error"):
+                ref = c1["cpu_ref_inmem_all_cores"]
+                hostinc["cpu_ref_inmem_all_cores"] = {k: ref.get(k) for k in ("value", "unit", "cores")}
             line["host_inclusive"] = hostinc
         if sweep_entries is not None:
             line["sweep"] = sweep_entries
@@ -1201,7 +1309,7 @@ def main():
         dist.destroy_process_group()
     if not checks_ok:
         bad = [c["rank"] for c in per_rank_checks if not parity_ok(c["parity"], c["corruption_drill"])]
-        bad_sweep = [e["key"] for e in (multi_entries or []) if not e.get("checks_all_ranks_pass")]
+        bad_sweep = [e["key"] for e in (multi_entries or []) if "skipped" not in e and not e.get("checks_all_ranks_pass")]
         print(f"bench: parity or corruption drill failed: headline rank(s) {bad}, sweep_multi {bad_sweep}",
               file=sys.stderr)
         sys.exit(3)

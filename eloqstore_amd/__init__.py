@@ -292,7 +292,7 @@ def flip_byte(pages, page_size: int, n: int, every: int, byte_offset: int = 10, 
 
 def stream_read(buf, nbytes: int, out, stream=None) -> None:
     """pcs_stream_read_dev: plain streaming read of nbytes (the read ceiling);
-    out receives one folded u64 per 64 KiB window."""
+    out receives one folded u64 per 4 KiB page (ceil(nbytes / 4096) words)."""
     _call("pcs_stream_read_dev", _ptr(buf), nbytes, _ptr(out), _stream(stream))
 
 

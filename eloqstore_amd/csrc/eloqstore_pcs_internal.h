@@ -51,7 +51,7 @@ int set_tuning(int key, int64_t value);
 bool take_tuning(int key);
 int64_t get_tuning(int key);
 // Plain streaming read of [buf, buf + bytes) (the HBM read ceiling): one
-// folded word per 64 KiB window into out[0 .. ceil(bytes / 65536)).
+// folded word per 4 KiB page into out[0 .. ceil(bytes / 4096)).
 hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s);
 
 // Pre-armed validate service (pcs_service_*): a mailbox in pinned host

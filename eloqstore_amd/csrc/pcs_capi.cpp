@@ -657,7 +657,8 @@ hipError_t event_wait_bounded(hipEvent_t ev, std::chrono::milliseconds limit) {
         const hipError_t q = hipEventQuery(ev);
         if (q != hipErrorNotReady) return q;
         if (std::chrono::steady_clock::now() - t0 > limit) return hipErrorNotReady;
-        std::this_thread::yield();
+        // gently: other threads' polls query the runtime too
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 
@@ -801,6 +802,7 @@ struct ServiceReq {
     uint32_t gen = 0;       // the generation it is posted to
     bool stamp = false;
     int relaunched = 0;
+    uint32_t checked_gen = 0;  // the service's generation at the last check
     int path = 0;           // PCS_PATH_* bits gathered so far
     bool quarantine = false;  // given up while its generation's kernel may still run
     Service::clock::time_point posted, checked;
@@ -916,6 +918,7 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
         r.seq = service_post_locked(sv, k, r.gen);
     }
     r.posted = r.checked = Service::clock::now();
+    r.checked_gen = r.gen;
     return PCS_OK;
 }
 
@@ -932,11 +935,13 @@ int service_progress(ServiceReq& r) {
         return 1;
     }
     // The kernel's state is checked every 50 µs, and at once when a newer
-    // generation has been started (this request must then be re-posted as
-    // soon as its own generation's kernel has left).
+    // generation has been started since the last check (this request must
+    // then be re-posted as soon as its own generation's kernel has left).
     const auto now = Service::clock::now();
-    if (now - r.checked < std::chrono::microseconds(50) && r.gen == sv.gen.load(std::memory_order_acquire)) return 0;
+    const uint32_t g_now = sv.gen.load(std::memory_order_acquire);
+    if (now - r.checked < std::chrono::microseconds(50) && g_now == r.checked_gen) return 0;
     r.checked = now;
+    r.checked_gen = g_now;
     // Never wait for the lock: its holder (another thread's submit, start,
     // stop or re-post) holds it for a launch at most, and this request is
     // looked at again on the next call.
@@ -1339,6 +1344,8 @@ int pcs_pages_validate_host_ex(const void* const* pages, uint64_t page_size, uin
         CallerGuard g(current_service(), page_size, n_pages, algo);
         const int r = service_run(g.service(), pages, page_size, n_pages, algo, ok, first_bad);
         if (r != kNotServed) return r;
+        t_path |= PCS_PATH_LAUNCHED;
+        return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);  // still counted as a caller (the guard): the gate sees both paths
     }
     t_path |= PCS_PATH_LAUNCHED;
     return host_batch(1, pages, page_size, n_pages, algo, ok, first_bad, nullptr);
@@ -1442,6 +1449,8 @@ int pcs_pages_stamp_host(void* const* pages, uint64_t page_size, uint64_t n_page
         CallerGuard g(current_service(), page_size, n_pages, algo);
         const int r = service_run(g.service(), cp, page_size, n_pages, algo, nullptr, nullptr);
         if (r != kNotServed) return r;
+        t_path |= PCS_PATH_LAUNCHED;
+        return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);  // still counted as a caller (the guard): the gate sees both paths
     }
     t_path |= PCS_PATH_LAUNCHED;
     return host_batch(2, cp, page_size, n_pages, algo, nullptr, nullptr, nullptr);

@@ -1207,50 +1207,55 @@ __global__ __launch_bounds__(256) void k_scatter_stamp_desc(uint8_t* __restrict_
     }
 }
 
-// Streaming-read ceiling: the fastest plain read of a device byte range found
-// (tools/lab/stream_lab.hip, profiles/r02/read_ceiling_lab.txt): one-shot
-// workgroups over contiguous 64 KiB windows in the kernels' tile order, the
-// product's lane layout (16-lane groups over 4 KiB slices, 16 nt dwordx4 loads
-// per lane issued before any is used), folded with xor/add into one word per
-// window.  7.2-7.3 TB/s over 4-32 GiB, insensitive to workgroups per CU (2-8)
-// and window size (32-128 KiB); the hash kernels on 4 KiB pages reach
-// 7.3-7.45 TB/s, i.e. they run AT the practical read ceiling of the part.
-constexpr uint64_t kStreamWin = 65536;
+// Streaming-read ceiling, built on k_xxh3_fixed<4096>'s exact
+// structure (round 5's 64 KiB-window reader ran ~4 % below
+// the hash kernel it was meant to bound): 256-thread blocks of 16 four-KiB
+// "pages", a 16-lane group each, loading xxh3_page_fixed<4096>'s chunks in its
+// order (chunk 0, then the other 15 dwordx4 non-temporal loads, all issued
+// before any is used), xcd_tile order over a grid that covers every tile
+// once, and the tile's 16 results staged in LDS and written as one 128-byte
+// non-temporal store.  Only the hash is gone: each lane folds its 16 pieces
+// with xor/add and the group xor-reduces them into the page's word.
+constexpr uint64_t kStreamPage = 4096;
 __global__ __launch_bounds__(256) void k_stream_read(const uint8_t* __restrict__ buf, uint64_t bytes,
                                                     uint64_t* __restrict__ out) {
-    const uint64_t nwin = (bytes + kStreamWin - 1) / kStreamWin;
-    const uint64_t w = xcd_tile(blockIdx.x, nwin);
+    __shared__ uint64_t tile_h[16];
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const uint8_t* win = buf + w * kStreamWin + 4096u * grp + 16u * g;
-    const uint64_t lim = bytes - w * kStreamWin;  // bytes of this window (full ones: >= 64 KiB)
-    u32x4 d[16];
+    const uint64_t npages = (bytes + kStreamPage - 1) / kStreamPage;
+    const uint64_t ntiles = (npages + 15) / 16;
+    const uint64_t t = xcd_tile(blockIdx.x, ntiles);
+    const uint64_t pg = t * 16 + grp;
+    if (pg < npages) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(buf + pg * kStreamPage) + g;
+        const uint64_t lim = bytes - pg * kStreamPage;  // bytes of this page (whole pages: >= 4096)
+        u32x4 d[16];
+        if (lim >= kStreamPage) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const uint64_t o = 4096u * grp + 256u * c + 16u * g;
-        d[c] = o + 16 <= lim ? ld16<true>(reinterpret_cast<const u32x4*>(win + 256u * c)) : u32x4{0, 0, 0, 0};
-    }
-    uint32_t x = 0, y = 0, z = 0, v = 0;
+            for (int c = 0; c < 16; ++c) d[c] = ld16<true>(base + c * 16);
+        } else {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        x ^= d[c].x;
-        y += d[c].y;
-        z ^= d[c].z;
-        v += d[c].w;
+            for (int c = 0; c < 16; ++c)
+                d[c] = 256u * c + 16u * g + 16 <= lim ? ld16<true>(base + c * 16) : u32x4{0, 0, 0, 0};
+        }
+        uint32_t x = 0, y = 0, z = 0, v = 0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            x ^= d[c].x;
+            y += d[c].y;
+            z ^= d[c].z;
+            v += d[c].w;
+        }
+        uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + v);
+        r ^= dpp64<kRowRor1>(r);
+        r ^= dpp64<kRowRor2>(r);
+        r ^= dpp64<kRowRor4>(r);
+        r ^= dpp64<kRowRor8>(r);
+        if (g == 0) tile_h[grp] = r;
     }
-    uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + v);
-    r ^= dpp64<kRowRor1>(r);
-    r ^= dpp64<kRowRor2>(r);
-    r ^= dpp64<kRowRor4>(r);
-    r ^= dpp64<kRowRor8>(r);
-    __shared__ uint64_t part[16];
-    if (g == 0) part[grp] = r;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) t ^= part[k];
-        st_nt(out + w, t);
-    }
+    const uint64_t i = t * 16 + threadIdx.x;
+    if (threadIdx.x < 16 && i < npages) st_nt(out + i, tile_h[threadIdx.x]);
+}
 }
 
 // ---------------------------------------------------------------------------
@@ -2005,9 +2010,9 @@ hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint
 
 hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hipStream_t s) {
     if (bytes < 16) return hipSuccess;
-    const uint64_t nwin = (bytes + kStreamWin - 1) / kStreamWin;
-    if (nwin > 0x7FFFFFFFull) return hipErrorNotSupported;
-    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)nwin), dim3(kBlock), 0, s, buf, bytes & ~uint64_t(15), out);
+    const uint64_t ntiles = ((bytes + kStreamPage - 1) / kStreamPage + 15) / 16;
+    if (ntiles > 0x7FFFFFFFull) return hipErrorNotSupported;
+    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)ntiles), dim3(kBlock), 0, s, buf, bytes & ~uint64_t(15), out);
     return hipGetLastError();
 }
 

@@ -92,7 +92,8 @@ enum pcs_flags {
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
  *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
  *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
- *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST (additive) */
+ *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST (additive); pcs_stream_read_dev writes
+ *      one word per 4 KiB (was per 64 KiB: size d_out for the new count) */
 #define PCS_ABI_VERSION 6
 int pcs_abi_version(void);
 const char *pcs_version(void);
@@ -417,12 +418,14 @@ int pcs_gen_desc_dev(void *d_base, const uint64_t *d_off, const uint32_t *d_len,
 int pcs_flip_byte_dev(void *d_pages, uint64_t page_size, uint64_t n_pages, uint64_t every,
                       uint64_t byte_offset, pcs_stream_t stream);
 /* Streaming-read ceiling: a plain read of [d_buf, d_buf + bytes) (16-byte
- * aligned; a trailing partial 16 bytes is ignored) with the fastest read
- * pattern measured (64 KiB windows per workgroup, XCD-contiguous order, nt
- * dwordx4 loads), folded into one word per 64 KiB window:
- * d_out[0 .. ceil(bytes / 65536)).  The roofline's measured companion: the
+ * aligned; a trailing partial 16 bytes is ignored) with the headline hash
+ * kernel's exact structure and load pattern (256-thread workgroups of 16 four-
+ * KiB "pages", XCD-contiguous tile order, nt dwordx4 loads, one 128-byte
+ * result store per tile) and no hash: each 4 KiB page folded into one word,
+ * d_out[0 .. ceil(bytes / 4096)).  The roofline's measured companion: the
  * hash kernels are compared with the rate at which the same bytes can merely
- * be read. */
+ * be read the same way.  (ABI 6: one word per 4 KiB; rounds 2-5 wrote one
+ * per 64 KiB window.) */
 int pcs_stream_read_dev(const void *d_buf, uint64_t bytes, uint64_t *d_out, pcs_stream_t stream);
 
 #ifdef __cplusplus

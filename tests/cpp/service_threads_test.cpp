@@ -44,6 +44,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <functional>
 #include <map>
 #include <string>
 #include <chrono>
@@ -212,6 +213,7 @@ void print_attribution(std::vector<Sample>& all) {
 struct PollStats {
     uint64_t polls = 0, over = 0;
     double max_us = 0, fallback_us = 0;
+    std::vector<float> top;  // the slowest polls (fallback poll excluded), slowest first
 };
 PollStats poll_timed(pcs_batch* b, double limit_s) {
     PollStats st;
@@ -228,6 +230,11 @@ PollStats poll_timed(pcs_batch* b, double limit_s) {
         } else {
             st.max_us = std::max(st.max_us, us);
             st.over += us > 100.0;
+            if (st.top.size() < 5 || us > st.top.back()) {
+                st.top.push_back((float)us);
+                std::sort(st.top.begin(), st.top.end(), std::greater<float>());
+                if (st.top.size() > 5) st.top.pop_back();
+            }
         }
         if (x == 1) return st;
         CHECK(Clock::now() < end);
@@ -235,6 +242,16 @@ PollStats poll_timed(pcs_batch* b, double limit_s) {
 }
 
 // n pages of the pool from page `first`, page k corrupted; submit + return
+std::string top_polls(const PollStats& st) {
+    std::string s;
+    char b[32];
+    for (float x : st.top) {
+        std::snprintf(b, sizeof b, "%s%.1f", s.empty() ? "" : " ", x);
+        s += b;
+    }
+    return s;
+}
+
 std::vector<const void*> bad_batch(char* pool, size_t first, size_t n, size_t k) {
     std::vector<const void*> v;
     for (size_t i = 0; i < n; ++i) v.push_back(pool + (first + i) * P);
@@ -283,9 +300,10 @@ int slow_stop(char* pool) {
     CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_MAX_CALLERS, 2) == PCS_OK);
     const int path = pcs_batch_path(b);
     std::printf("slow stop: pcs_service_stop rc %d in %.1f ms (kernel exit delay %lld ms); batch done after %.1f ms "
-                "of polls: %llu polls, max %.1f us, %llu over 100 us (the re-launching poll: %.1f us); path %s\n",
+                "of polls: %llu polls, max %.1f us (slowest: %s), %llu over 100 us (the re-launching poll: %.1f us); "
+                "path %s\n",
                 stop_rc.load(), stop_ms.load(), (long long)kExitUs / 1000, poll_ms, (unsigned long long)st.polls,
-                st.max_us, (unsigned long long)st.over, st.fallback_us, path_bits(path).c_str());
+                st.max_us, top_polls(st).c_str(), (unsigned long long)st.over, st.fallback_us, path_bits(path).c_str());
     CHECK(stop_rc == PCS_OK);
     CHECK(stop_ms >= 0.8 * kExitUs / 1000);  // the stop really waited for the slow kernel ...
     CHECK(poll_ms >= 0.8 * kExitUs / 1000);  // ... and the batch was polled all that time
@@ -334,9 +352,10 @@ int slow_timeout(char* pool) {
     CHECK(pcs_batch_wait(b) == PCS_OK);
     const int s_path = pcs_batch_path(b);
     check_result(b, v, 7);
-    std::printf("slow timeout: request gave up after %.2f s (%llu polls, max %.1f us, %llu over 100 us, re-launching "
-                "poll %.1f us), path %s; while quarantined: %s; after the kernel left: %s\n",
-                gave_up_s, (unsigned long long)st.polls, st.max_us, (unsigned long long)st.over, st.fallback_us,
+    std::printf("slow timeout: request gave up after %.2f s (%llu polls, max %.1f us (slowest: %s), %llu over 100 us, "
+                "re-launching poll %.1f us), path %s; while quarantined: %s; after the kernel left: %s\n",
+                gave_up_s, (unsigned long long)st.polls, st.max_us, top_polls(st).c_str(), (unsigned long long)st.over,
+                st.fallback_us,
                 path_bits(path).c_str(), path_bits(q_path).c_str(), path_bits(s_path).c_str());
     CHECK(s_path & PCS_PATH_SERVED);
     CHECK(pcs_service_stop() == PCS_OK);

@@ -19,7 +19,8 @@ SWEEP_KEYS = ["config3_xxh3", "config3_xxh64", "config4_xxh3", "config5_xxh3", "
 
 def test_bench_line_and_sweep():
     r = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--pages-per-gpu", "65536",
-                        "--sweep-steps", "3", "--sweep-warmup", "1", "--sweep-scale", "16", "--no-cpu-baseline"],
+                        "--sweep-steps", "3", "--sweep-warmup", "1", "--sweep-scale", "16", "--no-cpu-baseline",
+                        "--no-host-inclusive"],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -34,6 +35,13 @@ def test_bench_line_and_sweep():
     assert d["parity"]["mismatches"] == 0 and d["parity"]["pages"] > 0
     assert d["corruption_drill"]["pass"]
     assert d["stream_read_GBps"] > 0
+    # the ceiling and the hash kernel under one protocol
+    ceil = d["ceiling"]
+    assert ceil["stream_read_GBps"] == d["stream_read_GBps"] and 0.5 < ceil["frac_of_ceiling"] < 1.5, ceil
+    assert roof["frac_of_ceiling"] > 0
+    # the driver's protocol at process start, before the settle
+    assert d["cold"]["value"] > 0 and d["cold"]["steps"] == 5 and d["cold"]["warmup"] == 2 and d["cold"]["frac"] > 0
+    assert "host_inclusive" not in d
     # untimed steps ran for the default 1.5 s before the warmup
     assert d["settle"]["ms"] == 1500.0 and d["settle"]["steps"] >= 8 and d["settle"]["steps"] % 8 == 0
     assert [e["key"] for e in d["sweep"]] == SWEEP_KEYS
@@ -82,7 +90,19 @@ def test_bench_line_survives_failing_config1():
     assert "PCS_BENCH_FAIL_CONFIG1" in d["config1_error"]
     assert d["cpu_baseline"] is None
     assert d["roofline"]["frac"] > 0 and d["parity"]["mismatches"] == 0
-    assert d["host_inclusive"]["direct_pinned_digests_match_device"]
+    hi = d["host_inclusive"]
+    assert hi["parity_mismatches"] == 0 and set(hi["legs"]) == {"direct_pinned", "gather_pageable",
+                                                                "gather_scattered", "zero_copy_scattered"}
+    for leg in hi["legs"].values():
+        assert leg["GiBps"] > 0 and 0 < leg["frac_of_pcie"] < 1.5 and leg["parity_mismatches"] == 0, leg
+
+
+def test_host_inclusive_runs_by_default():
+    """VERDICT r05 #3: the N=1 line carries the host-inclusive legs by default."""
+    d = _one_line(subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--pages-per-gpu",
+                                  "65536", "--no-sweep", "--no-cpu-baseline", "--no-live-traffic"], cwd=ROOT,
+                                 capture_output=True, text=True, timeout=300))
+    assert d["host_inclusive"]["parity_mismatches"] == 0 and d["host_inclusive"]["pages"] == 65536
 
 
 def test_bench_wall_budget_skips_optional_legs():

@@ -504,33 +504,34 @@ def test_full_size_64k_chunks_sampled():
 
 
 def _stream_fold(buf: np.ndarray) -> np.ndarray:
-    """What pcs_stream_read_dev computes per 64 KiB window: lane (group k,
-    lane g) folds its 16 pieces (bytes 4096k + 256c + 16g) with xor/add, lanes
-    and groups xor-reduced; a partial window reads only its whole 16 B pieces."""
+    """What pcs_stream_read_dev computes per 4 KiB page: lane g of the page's
+    group folds its 16 pieces (bytes 256c + 16g) with xor/add, the 16 lanes
+    xor-reduced; a partial page reads only its whole 16 B pieces."""
     nbytes = buf.nbytes - buf.nbytes % 16
-    nwin = (nbytes + 65535) // 65536
-    pad = np.zeros(nwin * 65536, dtype=np.uint8)
+    npg = (nbytes + 4095) // 4096
+    pad = np.zeros(npg * 4096, dtype=np.uint8)
     pad[:nbytes] = buf[:nbytes]
-    w = pad.view(np.uint32).reshape(nwin, 16, 16, 16, 4)  # window, group, chunk c, lane g, word
-    x = np.bitwise_xor.reduce(w[..., 0], axis=2).astype(np.uint64)
-    y = w[..., 1].astype(np.uint64).sum(axis=2) & 0xFFFFFFFF
-    z = np.bitwise_xor.reduce(w[..., 2], axis=2).astype(np.uint64)
-    ww = w[..., 3].astype(np.uint64).sum(axis=2) & 0xFFFFFFFF
+    w = pad.view(np.uint32).reshape(npg, 16, 16, 4)  # page, chunk c, lane g, word
+    x = np.bitwise_xor.reduce(w[..., 0], axis=1).astype(np.uint64)
+    y = w[..., 1].astype(np.uint64).sum(axis=1) & 0xFFFFFFFF
+    z = np.bitwise_xor.reduce(w[..., 2], axis=1).astype(np.uint64)
+    ww = w[..., 3].astype(np.uint64).sum(axis=1) & 0xFFFFFFFF
     r = ((x ^ z) << np.uint64(32)) | ((y + ww) & np.uint64(0xFFFFFFFF))
-    return np.bitwise_xor.reduce(r.reshape(nwin, -1), axis=1)
+    return np.bitwise_xor.reduce(r, axis=1)
 
 
-@pytest.mark.parametrize("nbytes", [16, 4096, 65536, 65536 * 7, 65536 * 300 + 4096 + 48, 65536 * 5 + 23])
+@pytest.mark.parametrize("nbytes", [16, 4096, 65536, 65536 * 7, 65536 * 300 + 4096 + 48, 65536 * 5 + 23,
+                                    4096 * 17 + 4000])
 def test_stream_read_fold(nbytes):
     """The read-ceiling kernel reads every (whole 16-byte piece of every) byte
-    of the range exactly once, full and partial windows alike."""
+    of the range exactly once, whole and partial pages and tiles alike."""
     host = np.random.default_rng(nbytes).integers(0, 256, size=nbytes, dtype=np.uint8)
     buf = torch.from_numpy(host).to(DEV)
-    nwin = (nbytes - nbytes % 16 + 65535) // 65536
-    out = torch.zeros(nwin + 1, dtype=torch.int64, device=DEV)
+    npg = (nbytes - nbytes % 16 + 4095) // 4096
+    out = torch.zeros(npg + 1, dtype=torch.int64, device=DEV)
     pcs.stream_read(buf, nbytes, out)
     got = u64(out)
-    assert np.array_equal(got[:nwin], _stream_fold(host)) and got[nwin] == 0
+    assert np.array_equal(got[:npg], _stream_fold(host)) and got[npg] == 0
 
 
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])

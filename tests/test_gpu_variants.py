@@ -23,6 +23,10 @@ VARIANTS = {
     "grid_stride": {pcs.TUNE_XXH3_BLOCKS_PER_CU: 1, pcs.TUNE_XXH64_BLOCKS_PER_CU: 1},
     "x64_depth1": {pcs.TUNE_XXH64_LAYOUT: 2},
     "x64_depth4": {pcs.TUNE_XXH64_LAYOUT: 4},
+    # depth 3 (layout 5): the only depth that is not a power of two, so segment
+    # counts that are not a multiple of 3 leave through the in-loop break
+    "x64_depth3": {pcs.TUNE_XXH64_LAYOUT: 5},
+    "x64_two_waves_depth3": {pcs.TUNE_XXH64_WAVES: 2, pcs.TUNE_XXH64_LAYOUT: 5},
     "rt_one_block": {pcs.TUNE_XXH3_RT_BATCH: 0},
     "no_split": {pcs.TUNE_XXH3_SPLIT_PAGES: 0},
     "split_16k": {pcs.TUNE_XXH3_SPLIT_PAGES: 16384},
@@ -66,7 +70,7 @@ def test_variant_pages(tuned, P, n, algo):
 
 
 @pytest.mark.parametrize("tuned", ["default", "no_nt", "rt_one_block", "x64_depth1", "x64_depth4", "x64_one_wave",
-                                   "x64_two_waves_depth4"],
+                                   "x64_two_waves_depth4", "x64_depth3", "x64_two_waves_depth3"],
                          indirect=True)
 @pytest.mark.parametrize("algo", [pcs.XXH3_64, pcs.XXH64])
 def test_variant_mixed_desc(tuned, algo):

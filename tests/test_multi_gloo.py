@@ -106,3 +106,63 @@ def test_init_dist_keeps_stdout_to_the_json_line(tmp_path):
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines() == ['{"max_rank": 2}'], r.stdout
+
+
+def sweep_worker(rank: int, world: int, port: int, out_dir: str):
+    """bench.multi_rank_sweep under gloo with a stand-in workload (no GPU):
+    rank 1 raises inside config 7's TIMED launches.  Both ranks must leave
+    the sweep (no rank left waiting in a collective), record config 7 as an
+    error, and still run config 4."""
+    import json
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    class Ev:
+        def record(self):
+            pass
+
+        def elapsed_time(self, other):
+            return 1.0
+
+    class FakeWorkload:
+        def __init__(self, cfg, algo, rank_, n, dev):
+            self.cfg, self.n, self.bytes, self.desc, self.calls = cfg, n, n * 4096, f"fake config{cfg}", 0
+
+        def step(self, mode):
+            self.calls += 1
+            if self.cfg == 7 and rank == 1 and self.calls > 1:  # past the one warmup step
+                raise RuntimeError("fault in the timed launches")
+
+        def algorithmic_bytes(self, mode):
+            return self.bytes
+
+        def corruption_drill(self):
+            return {"pass": True}
+
+        def free(self):
+            pass
+
+    torch.cuda.synchronize = lambda *a: None
+    torch.cuda.Event = lambda enable_timing=True: Ev()
+    bench.Workload = FakeWorkload
+    bench.settle = lambda w, mode, ms: 0
+    bench.parity_sample = lambda w, mode="digest": {"pages": 1, "mismatches": 0}
+    out = bench.multi_rank_sweep(dist, world, rank, "cpu", 0, 3, 1, 1, 0.0, None)
+    late = bench.multi_rank_sweep(dist, world, rank, "cpu", 0, 3, 1, 1, 0.0, 0.0)
+    with open(os.path.join(out_dir, f"sweep{rank}.json"), "w") as f:
+        json.dump({"out": out, "late": late}, f)
+    dist.destroy_process_group()
+
+
+def test_multi_rank_sweep_survives_a_failing_rank(tmp_path):
+    import json
+
+    mp.spawn(sweep_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = json.load(open(tmp_path / f"sweep{r}.json"))
+        assert [e["key"] for e in d["out"]] == ["config7_xxh3", "config4_xxh3"]
+        assert "error" in d["out"][0] and "checks_all_ranks_pass" not in d["out"][0]
+        assert d["out"][1]["checks_all_ranks_pass"] and d["out"][1]["value"] > 0
+        assert all("skipped" in e for e in d["late"])

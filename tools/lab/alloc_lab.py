@@ -54,7 +54,7 @@ def main():
             continue
         bufs.append((f"contig#{i}", p.value, None))
     out = torch.empty(n, dtype=torch.int64, device="cuda:0")
-    scratch = torch.empty((nbytes + 65535) // 65536, dtype=torch.int64, device="cuda:0")
+    scratch = torch.empty((nbytes + 4095) // 4096, dtype=torch.int64, device="cuda:0")
     for name, ptr, _ in bufs:
         pcs.gen_pages(ptr, P, n, 0x5EED0005, 0)
     torch.cuda.synchronize()
