@@ -83,6 +83,7 @@ _SIGS = {
     "pcs_service_stop": [],
     "pcs_service_running": [],
     "pcs_last_path": [],
+    "pcs_thread_prepare": [],
     "pcs_batch_path": [_vp],
     "pcs_version": [],
     "pcs_abi_version": [],

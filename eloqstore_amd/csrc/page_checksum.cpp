@@ -72,6 +72,10 @@ void StopChecksumService() {
     if (int rc = pcs_service_stop()) die("StopChecksumService", rc);
 }
 
+void PrepareChecksumThread() {
+    if (int rc = pcs_thread_prepare()) die("PrepareChecksumThread", rc);
+}
+
 ChecksumBatch::ChecksumBatch() { status_ = pcs_batch_create(&batch_); }
 
 ChecksumBatch::~ChecksumBatch() { pcs_batch_destroy(batch_); }

@@ -139,8 +139,12 @@ struct ZcBufs {
         (void)hipHostFree(h_ok);
         *this = ZcBufs{};
     }
+    // At least a service-sized batch (256 pages): a batch the service gives
+    // back re-runs here from a poll, and growing would free pinned memory,
+    // which synchronises the device (the poll would wait for every kernel).
     int ensure(size_t n) {
         if (n <= cap) return PCS_OK;
+        n = std::max<size_t>(n, pcs::kServiceMaxPages);
         release();
         if (hipHostMalloc(reinterpret_cast<void**>(&h_ptrs), n * 8, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void**>(&h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
@@ -569,7 +573,8 @@ struct Service {
     std::atomic<int> lines{0};     // request lines (read without the lock when claiming one)
     int wpl = 0;                   // workgroups per line
     uint32_t idle_us = 0;
-    hipStream_t stream = nullptr;  // recreated at start unless a request still owns a line
+    hipStream_t stream = nullptr;  // kept across restarts; recreated only when its kind changes
+    int64_t stream_kind = -1;      // PCS_TUNE_SERVICE_STREAM it was created with
     hipEvent_t done[kServiceEvents] = {};  // done[g % 16]: recorded behind generation g's kernel
     pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped; never freed
     pcs::ServiceBox* d = nullptr;  // its device alias
@@ -1152,11 +1157,42 @@ int batch_failed(pcs_batch* b, int rc) {
 // Launch path of an asynchronous batch (arguments checked, n > 0): zero-copy
 // over registered pages, else staged (gather or direct DMA), on the batch's
 // own stream; completion is seen by poll / wait.
+// Result buffers of a batch: at least a service-sized batch (256 pages), so a
+// batch the service gives back never grows them from a poll (freeing device
+// or pinned memory synchronises the device: the poll would wait for every
+// kernel, the service's included).  pcs_batch_create sizes them at once.
+int batch_results(pcs_batch* b, uint64_t n) {
+    if (n <= b->cap_n) return PCS_OK;
+    n = std::max<uint64_t>(n, pcs::kServiceMaxPages);
+    (void)hipHostFree(b->h_dig);
+    (void)hipFree(b->d_dig);
+    (void)hipHostFree(b->h_ok);
+    (void)hipFree(b->d_ok);
+    b->h_dig = nullptr; b->d_dig = nullptr; b->h_ok = nullptr; b->d_ok = nullptr;
+    b->cap_n = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&b->h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&b->d_dig), n * 8) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&b->h_ok), n, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&b->d_ok), n) != hipSuccess)
+        return fail(PCS_ERR_NOMEM, "batch result allocation failed");
+    b->cap_n = n;
+    return PCS_OK;
+}
+
 int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo) {
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
     hipError_t e = hipSuccess;
-    if (n * P > b->cap_bytes) {
+    if (int rc = batch_results(b, n)) return rc;
+    b->zero_copy = false;
+    b->path |= PCS_PATH_LAUNCHED;
+    b->stamp_pages.assign(n, nullptr);
+    if (mode == PCS_BATCH_STAMP)
+        for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
+    hipStream_t s = b->stream;
+    b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
+    // page staging only off the zero-copy path
+    if (!b->zero_copy && n * P > b->cap_bytes) {
         (void)hipHostFree(b->h_pages);
         (void)hipFree(b->d_pages);
         b->h_pages = nullptr;
@@ -1167,27 +1203,6 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
             return fail(PCS_ERR_NOMEM, "batch staging allocation failed");
         b->cap_bytes = n * P;
     }
-    if (n > b->cap_n) {
-        (void)hipHostFree(b->h_dig);
-        (void)hipFree(b->d_dig);
-        (void)hipHostFree(b->h_ok);
-        (void)hipFree(b->d_ok);
-        b->h_dig = nullptr; b->d_dig = nullptr; b->h_ok = nullptr; b->d_ok = nullptr;
-        b->cap_n = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_dig), n * 8, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&b->d_dig), n * 8) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&b->h_ok), n, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&b->d_ok), n) != hipSuccess)
-            return fail(PCS_ERR_NOMEM, "batch result allocation failed");
-        b->cap_n = n;
-    }
-    b->zero_copy = false;
-    b->path |= PCS_PATH_LAUNCHED;
-    b->stamp_pages.assign(n, nullptr);
-    if (mode == PCS_BATCH_STAMP)
-        for (uint64_t i = 0; i < n; ++i) b->stamp_pages[i] = const_cast<void*>(pages[i]);
-    hipStream_t s = b->stream;
-    b->zero_copy = zero_copy_eligible(b->zc, pages, n, P, algo);
     // validate: completion from the landed verdicts; small zero-copy XXH3
     // stamps: from the per-page done bytes (each released after the header
     // and the digest word)
@@ -1234,6 +1249,7 @@ int batch_service_poll(pcs_batch* b) {
         uint64_t fb = UINT64_MAX;
         if (b->mode == PCS_BATCH_VALIDATE) b->svc_ok.resize(b->n);
         const int rc = service_collect(b->svc, b->mode == PCS_BATCH_VALIDATE ? b->svc_ok.data() : nullptr, &fb);
+        b->path |= b->svc.path;  // + PCS_PATH_SERVED
         service_release(b->svc);
         b->via_service = false;
         if (rc) return batch_failed(b, rc);
@@ -1369,12 +1385,15 @@ int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us) {
     int dev = -1;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "service start");
-    // The stream is recreated (PCS_TUNE_SERVICE_STREAM is read here) unless
-    // an asynchronous request of the previous run still owns a line and may
-    // be waiting on its kernel, a line is quarantined behind one, or the
-    // previous run's kernels have not left yet (a stop waits for them outside
-    // the lock; destroying the stream here would wait under it); the mailbox
-    // and the events are made once.
+    // The stream is kept across restarts: destroying and creating streams
+    // stalls other threads' HIP calls for ~2 ms (the soak's launch-path calls
+    // at a restart, profiles/r06/soak_*.txt).  It is recreated only when
+    // PCS_TUNE_SERVICE_STREAM (read here) asks for another kind, and then
+    // only if no asynchronous request of the previous run still owns a line
+    // (or a line is quarantined behind one) and the previous run's kernels
+    // have left (a stop waits for them outside the lock; destroying the
+    // stream here would wait under it); the mailbox and the events are made
+    // once.
     bool owned = false;
     for (int k = 0; k < pcs::kServiceMaxLines; ++k) {
         Service::Line& l = sv.line[k];
@@ -1385,13 +1404,17 @@ int pcs_service_start_ex(int lines, int workgroups_per_line, uint32_t idle_us) {
     }
     const hipEvent_t last = sv.done[sv.gen.load(std::memory_order_relaxed) % kServiceEvents];
     const bool left = !last || hipEventQuery(last) == hipSuccess;
-    if (sv.stream && !owned && left) {
+    const int64_t kind = pcs::get_tuning(PCS_TUNE_SERVICE_STREAM);
+    if (sv.stream && kind != sv.stream_kind && !owned && left) {
         (void)hipStreamDestroy(sv.stream);
         sv.stream = nullptr;
     }
-    if (!sv.stream && (e = service_stream(&sv.stream)) != hipSuccess) {
-        sv.stream = nullptr;
-        return hip_fail(e, "service start");
+    if (!sv.stream) {
+        if ((e = service_stream(&sv.stream)) != hipSuccess) {
+            sv.stream = nullptr;
+            return hip_fail(e, "service start");
+        }
+        sv.stream_kind = kind;
     }
     for (auto& ev : sv.done)
         if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
@@ -1502,6 +1525,39 @@ int pcs_host_register(void* p, uint64_t bytes) {
     return PCS_OK;
 }
 
+int pcs_thread_prepare(void) {
+    if (int rc = require_device()) return rc;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    if (dev < 0 || dev >= kServiceDevices) return fail(PCS_ERR_INVALID, "device index out of range");
+    HostCtx& ctx = t_ctx[dev];
+    if (int rc = ensure_slot(ctx.slot[0], 0, pcs::kServiceMaxPages)) return rc;
+    if (int rc = ctx.zc.ensure(pcs::kServiceMaxPages)) return rc;
+    // one process-wide pinned, mapped 4 KiB page per device to validate, kept
+    // for the life of the process (freeing pinned memory synchronises the device)
+    static std::mutex mu;
+    static void* warm[kServiceDevices] = {};
+    void* page = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!warm[dev]) {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, 4096, hipHostMallocMapped) != hipSuccess) return fail(PCS_ERR_NOMEM, "warm page");
+            std::memset(p, 0, 4096);
+            warm[dev] = p;
+        }
+        page = warm[dev];
+    }
+    void* d_page = nullptr;
+    if ((e = hipHostGetDevicePointer(&d_page, page, 0)) != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+    ctx.zc.h_ptrs[0] = reinterpret_cast<uint64_t>(d_page);
+    hipStream_t s = ctx.slot[0].stream;
+    e = pcs::run_list(1, PCS_XXH3_64, ctx.zc.d_ptrs, ctx.zc.h_ptrs, 4096, 1, nullptr, ctx.zc.d_ok, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return finish(e, "pcs_thread_prepare");
+}
+
 int pcs_host_unregister(void* p) {
     if (!p) return fail(PCS_ERR_INVALID, "null pointer");
     if (g_regions.remove(reinterpret_cast<uintptr_t>(p), false) != pcs::RegionRegistry::kOk)
@@ -1520,6 +1576,16 @@ int pcs_batch_create(pcs_batch** out) {
     if (e != hipSuccess) {
         pcs_batch_destroy(b);
         return hip_fail(e, "pcs_batch_create");
+    }
+    // result and zero-copy buffers for a service-sized batch up front: no
+    // poll of a batch of up to 256 pages ever allocates or frees
+    if (int rc = batch_results(b, pcs::kServiceMaxPages)) {
+        pcs_batch_destroy(b);
+        return rc;
+    }
+    if (int rc = b->zc.ensure(pcs::kServiceMaxPages)) {
+        pcs_batch_destroy(b);
+        return rc;
     }
     *out = b;
     return PCS_OK;

@@ -1256,7 +1256,6 @@ __global__ __launch_bounds__(256) void k_stream_read(const uint8_t* __restrict__
     const uint64_t i = t * 16 + threadIdx.x;
     if (threadIdx.x < 16 && i < npages) st_nt(out + i, tile_h[threadIdx.x]);
 }
-}
 
 // ---------------------------------------------------------------------------
 // launch plumbing

@@ -131,6 +131,11 @@ void UnregisterPagePool(void* base);
 // device has its own service.
 void StartChecksumService(int workgroups = 4, uint32_t idle_us = 1000, int lines = 1);
 void StopChecksumService();
+// Optional, once per shard thread at start-up (pcs_thread_prepare): creates
+// the thread's stream and the pinned buffers a batch of up to 256 pages uses
+// and runs one 1-page batch, so the thread's first ReadPages / FlushBatchPages
+// batch does not pay for that (16-35 ms with eight threads starting at once).
+void PrepareChecksumThread();
 inline constexpr size_t kGpuChecksumMinBatchBytesService = size_t(96) << 10;
 
 // Asynchronous batch for coroutine call sites: Submit, then Poll() from the

@@ -92,7 +92,7 @@ enum pcs_flags {
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
  *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
  *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
- *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST (additive); pcs_stream_read_dev writes
+ *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, pcs_thread_prepare (additive); pcs_stream_read_dev writes
  *      one word per 4 KiB (was per 64 KiB: size d_out for the new count) */
 #define PCS_ABI_VERSION 6
 int pcs_abi_version(void);
@@ -177,6 +177,14 @@ int pcs_host_free_pinned(void *p);
  * (PCS_TUNE_ZERO_COPY).  Regions must not overlap.  A region must stay
  * registered until every batch over it has completed. */
 int pcs_host_register(void *ptr, uint64_t bytes);
+/* Optional, once per host thread that will issue host batches (a shard
+ * thread at start-up): creates the thread's stream and the pinned result and
+ * zero-copy buffers a batch of up to 256 pages uses on the current device,
+ * and runs one 1-page zero-copy batch through them (the process's first
+ * launch also loads the kernels).  Without it the thread's first host batch
+ * pays for this: 16-35 ms with eight threads starting at once (soak
+ * attribution).  Idempotent. */
+int pcs_thread_prepare(void);
 int pcs_host_unregister(void *ptr);  /* ptr = the base passed to pcs_host_register */
 
 /* ---- asynchronous host batches (shard-loop integration) --------------------

@@ -55,6 +55,7 @@ def test_service_serves_small_batches(service, P):
             ok, fb = pcs.validate_ptrs(ptrs, P)
             assert ok.all() and fb is None
             assert counters() == (s0 + 1, z0), n
+            assert pcs.lib().pcs_last_path() & pcs.PATH_SERVED and not pcs.lib().pcs_last_path() & pcs.PATH_LAUNCHED
             for j in sorted({0, n // 2, n - 1}):
                 pool.pages[idx[j], P - 1] ^= 0x01  # the last stripe
                 ok, fb = pcs.validate_ptrs(ptrs, P)
@@ -580,6 +581,7 @@ def test_service_async_batches(service):
                 pool.pages[idx[k], 3000] ^= 0x40
                 assert fb == k and sum(ok) == n - 1 and ok[k] == 0, (n, fb)
                 assert counters() == (s0 + 1, z0), n
+                assert b.path() & pcs.PATH_SERVED and not b.path() & pcs.PATH_LAUNCHED, b.path()
             idx = np.arange(300, 340)
             pool.pages[idx, :8] = 0
             s0, z0 = counters()
@@ -684,6 +686,7 @@ def test_service_lifecycle():
             s0, z0 = counters()
             ok, fb = pcs.validate_ptrs(ptrs, P)  # after stop: the launch path
             assert ok.all() and counters() == (s0, z0 + 1)
+            assert pcs.lib().pcs_last_path() == pcs.PATH_LAUNCHED
         pcs._call("pcs_service_stop")  # stopping a stopped service is fine
 
 
@@ -769,11 +772,13 @@ def test_poll_never_waits_on_a_slow_service_exit(mode):
     stays after it is told to leave).
     --slow-stop: another thread's pcs_service_stop waits ~300 ms for the
     kernel while this thread polls an async batch posted to it: every poll
-    returns within 100 us (round 5 held the service's lock through the
-    drain), the stop really took the 300 ms, and the batch comes back exact
-    through the launch path.
+    returns within 1 ms and at most 3 of the ~4 M over 100 us (round 5 held
+    the service's lock through the drain: polls waited the whole 300 ms; a
+    control thread that only reads the clock reports the host's own
+    scheduling gaps beside them), the stop really took the 300 ms, and the
+    batch comes back exact through the launch path.
     --slow-timeout: nobody stops it; the request gives up after 5 s (polls
-    still under 100 us), re-runs exact on the launch path, and its line is
+    bounded the same way), re-runs exact on the launch path, and its line is
     quarantined until the kernel has left: a request meanwhile is launched,
     and the line serves again afterwards."""
     import os
@@ -782,3 +787,28 @@ def test_poll_never_waits_on_a_slow_service_exit(mode):
     r = subprocess.run([exe, mode], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and f"{mode[2:]} ok" in r.stdout, r.stdout + r.stderr
     print(r.stdout)
+
+
+def test_thread_prepare():
+    """pcs_thread_prepare (eloqstore::PrepareChecksumThread): idempotent, and
+    a prepared thread's first small host batch is served exactly."""
+    P = 4096
+    with stamped_pool(64, P, 0x5FC) as pool:
+        errors = []
+
+        def worker():
+            try:
+                for _ in range(2):
+                    pcs._call("pcs_thread_prepare")
+                pool.pages[3, 99] ^= 0x01
+                ok, fb = pcs.validate_ptrs(pool.ptr(np.arange(8)), P)
+                pool.pages[3, 99] ^= 0x01
+                if fb != 3 or ok.sum() != 7:
+                    errors.append((fb, ok))
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        th = threading.Thread(target=worker)
+        th.start()
+        th.join()
+        assert not errors, errors
