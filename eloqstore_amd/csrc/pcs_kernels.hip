@@ -1216,9 +1216,18 @@ __global__ __launch_bounds__(256) void k_scatter_stamp_desc(uint8_t* __restrict_
 // once, and the tile's 16 results staged in LDS and written as one 128-byte
 // non-temporal store.  Only the hash is gone: each lane folds its 16 pieces
 // with xor/add and the group xor-reduces them into the page's word.
+// Occupancy: with 72 VGPRs this body would run 7 waves per SIMD and read
+// 3-4 % slower than the hash kernel (4 waves, 120 VGPRs); over 1-7 waves per
+// SIMD a plain read of 4 KiB pages is fastest at 2 (7.40 TB/s on 4 GiB, 7.42
+// on 32 GiB: tools/lab/occupancy_lab.hip, profiles/r06/occupancy_lab_r06e.txt),
+// so run_stream_read caps it there with dynamic LDS (kStreamLdsPad bytes per
+// workgroup: two workgroups per CU).  The ceiling is the best plain read of
+// these bytes found, not the reader at one arbitrary occupancy.
 constexpr uint64_t kStreamPage = 4096;
+constexpr size_t kStreamLdsPad = 163840 / 2 - 2048;
 __global__ __launch_bounds__(256) void k_stream_read(const uint8_t* __restrict__ buf, uint64_t bytes,
                                                     uint64_t* __restrict__ out) {
+    extern __shared__ uint64_t occupancy_pad[];  // allocated for the cap, never used
     __shared__ uint64_t tile_h[16];
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const uint64_t npages = (bytes + kStreamPage - 1) / kStreamPage;
@@ -1255,6 +1264,7 @@ __global__ __launch_bounds__(256) void k_stream_read(const uint8_t* __restrict__
     __syncthreads();
     const uint64_t i = t * 16 + threadIdx.x;
     if (threadIdx.x < 16 && i < npages) st_nt(out + i, tile_h[threadIdx.x]);
+    if (bytes == 0) occupancy_pad[threadIdx.x] = 0;  // never taken (bytes >= 16): keeps the array
 }
 
 // ---------------------------------------------------------------------------
@@ -2011,7 +2021,15 @@ hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hi
     if (bytes < 16) return hipSuccess;
     const uint64_t ntiles = ((bytes + kStreamPage - 1) / kStreamPage + 15) / 16;
     if (ntiles > 0x7FFFFFFFull) return hipErrorNotSupported;
-    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)ntiles), dim3(kBlock), 0, s, buf, bytes & ~uint64_t(15), out);
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_stream_read),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsPad);
+    });
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)ntiles), dim3(kBlock), kStreamLdsPad, s, buf,
+                       bytes & ~uint64_t(15), out);
     return hipGetLastError();
 }
 
