@@ -230,6 +230,9 @@ struct PollStats {
     double max_us = 0, fallback_us = 0;
     double control_max_us = 0;  // the largest gap a bare clock-read loop saw meanwhile (scheduler noise)
     uint64_t control_over = 0;  // its gaps over 100 us
+    // polls over 100 us that no control gap overlaps (the library's own), and the largest of them
+    uint64_t unexplained = 0;
+    double unexplained_max_us = 0;
     std::vector<float> top;  // the slowest polls (fallback poll excluded), slowest first
 };
 PollStats poll_timed(pcs_batch* b, double limit_s) {
@@ -238,13 +241,20 @@ PollStats poll_timed(pcs_batch* b, double limit_s) {
     // control: a thread that only reads the clock, over the same window; a
     // gap it sees is the host's scheduling noise, not this library
     std::atomic<bool> stop{false};
+    using Span = std::pair<Clock::time_point, Clock::time_point>;
+    std::vector<Span> gaps, slow;  // control gaps / polls over 100 us
+    gaps.reserve(100000);
+    slow.reserve(100000);
     std::thread control([&] {
         auto prev = Clock::now();
         while (!stop.load(std::memory_order_relaxed)) {
             const auto now = Clock::now();
             const double gap = std::chrono::duration<double, std::micro>(now - prev).count();
             st.control_max_us = std::max(st.control_max_us, gap);
-            st.control_over += gap > 100.0;
+            if (gap > 100.0) {
+                ++st.control_over;
+                if (gaps.size() < gaps.capacity()) gaps.push_back({prev, now});
+            }
             prev = now;
         }
     });
@@ -253,14 +263,28 @@ PollStats poll_timed(pcs_batch* b, double limit_s) {
         std::thread& th;
         ~Join() {
             stop = true;
-            th.join();
+            if (th.joinable()) th.join();
         }
     } join{stop, control};
+    // a slow poll that overlaps a gap the control thread saw too is the host
+    // descheduling the process (throttling, preemption), not the library
+    auto attribute = [&] {
+        for (const Span& p : slow) {
+            bool seen = false;
+            for (const Span& g : gaps) seen |= g.first < p.second && p.first < g.second;
+            if (!seen) {
+                ++st.unexplained;
+                st.unexplained_max_us =
+                    std::max(st.unexplained_max_us, std::chrono::duration<double, std::micro>(p.second - p.first).count());
+            }
+        }
+    };
     for (;;) {
         const int before = pcs_batch_path(b);
         const auto t0 = Clock::now();
         const int x = pcs_batch_poll(b);
-        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        const auto t1 = Clock::now();
+        const double us = std::chrono::duration<double, std::micro>(t1 - t0).count();
         CHECK(x >= 0);
         ++st.polls;
         if (!(before & PCS_PATH_FALLBACK) && (pcs_batch_path(b) & PCS_PATH_FALLBACK)) {
@@ -268,13 +292,19 @@ PollStats poll_timed(pcs_batch* b, double limit_s) {
         } else {
             st.max_us = std::max(st.max_us, us);
             st.over += us > 100.0;
+            if (us > 100.0 && slow.size() < slow.capacity()) slow.push_back({t0, t1});
             if (st.top.size() < 5 || us > st.top.back()) {
                 st.top.push_back((float)us);
                 std::sort(st.top.begin(), st.top.end(), std::greater<float>());
                 if (st.top.size() > 5) st.top.pop_back();
             }
         }
-        if (x == 1) return st;
+        if (x == 1) {
+            stop = true;
+            control.join();
+            attribute();
+            return st;
+        }
         CHECK(Clock::now() < end);
     }
 }
@@ -339,19 +369,22 @@ int slow_stop(char* pool) {
     const int path = pcs_batch_path(b);
     std::printf("slow stop: pcs_service_stop rc %d in %.1f ms (kernel exit delay %lld ms); batch done after %.1f ms "
                 "of polls: %llu polls, max %.1f us (slowest: %s), %llu over 100 us (the re-launching poll: %.1f us); "
-                "control thread: max gap %.1f us, %llu gaps over 100 us; path %s\n",
+                "control thread: max gap %.1f us, %llu gaps over 100 us; slow polls no control gap explains: %llu "
+                "(max %.1f us); path %s\n",
                 stop_rc.load(), stop_ms.load(), (long long)kExitUs / 1000, poll_ms, (unsigned long long)st.polls,
                 st.max_us, top_polls(st).c_str(), (unsigned long long)st.over, st.fallback_us, st.control_max_us,
-                (unsigned long long)st.control_over, path_bits(path).c_str());
+                (unsigned long long)st.control_over, (unsigned long long)st.unexplained, st.unexplained_max_us,
+                path_bits(path).c_str());
     CHECK(stop_rc == PCS_OK);
     CHECK(stop_ms >= 0.8 * kExitUs / 1000);  // the stop really waited for the slow kernel ...
     CHECK(poll_ms >= 0.8 * kExitUs / 1000);  // ... and the batch was polled all that time
     CHECK((path & PCS_PATH_FALLBACK) && (path & PCS_PATH_LAUNCHED) && !(path & PCS_PATH_SERVED));
     check_result(b, v, 21);
-    // Round 5 blocked a poll for the whole 300 ms exit.  Bound: every poll
-    // within 1 ms, and at most 3 of the millions over 100 us (a host
-    // scheduling gap, which the control thread sees too).
-    CHECK(st.over <= 3 && st.max_us < 1000.0);
+    // Round 5 blocked a poll for the whole 300 ms exit.  Bound: at most 3 of
+    // the millions of polls over 100 us that the host's own descheduling
+    // (a gap the control thread saw at the same time) does not explain, and
+    // none of those over 1 ms.
+    CHECK(st.unexplained <= 3 && st.unexplained_max_us < 1000.0);
     CHECK(st.fallback_us < 2000.0);
     pcs_batch_destroy(b);
     return 0;
@@ -376,15 +409,17 @@ int slow_timeout(char* pool) {
     const double gave_up_s = std::chrono::duration<double>(Clock::now() - p0).count();
     const int path = pcs_batch_path(b);
     std::printf("slow timeout: gave up after %.2f s: %llu polls, max %.1f us (slowest: %s), %llu over 100 us, "
-                "re-launching poll %.1f us, control thread max gap %.1f us (%llu over 100 us), path %s\n", gave_up_s,
+                "re-launching poll %.1f us, control thread max gap %.1f us (%llu over 100 us), unexplained slow polls "
+                "%llu (max %.1f us), path %s\n", gave_up_s,
                 (unsigned long long)st.polls, st.max_us, top_polls(st).c_str(), (unsigned long long)st.over,
-                st.fallback_us, st.control_max_us, (unsigned long long)st.control_over, path_bits(path).c_str());
+                st.fallback_us, st.control_max_us, (unsigned long long)st.control_over,
+                (unsigned long long)st.unexplained, st.unexplained_max_us, path_bits(path).c_str());
     std::fflush(stdout);
     check_result(b, v, 44);
     CHECK((path & PCS_PATH_FALLBACK) && !(path & PCS_PATH_SERVED) && !(path & PCS_PATH_REPOSTED));
     CHECK(st.fallback_us < 2000.0);
     CHECK(gave_up_s >= 4.9 && gave_up_s < 6.0);
-    CHECK(st.over <= 3 && st.max_us < 1000.0);
+    CHECK(st.unexplained <= 3 && st.unexplained_max_us < 1000.0);
     // the line is quarantined until the slow kernel has left (~6 s after the
     // submit): a request now takes the launch path ...
     v = bad_batch(pool, 500, 8, 2);

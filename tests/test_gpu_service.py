@@ -771,12 +771,14 @@ def test_poll_never_waits_on_a_slow_service_exit(mode):
     a slow leaver (PCS_TUNE_SERVICE_SLOW_EXIT_TEST: it serves nothing and
     stays after it is told to leave).
     --slow-stop: another thread's pcs_service_stop waits ~300 ms for the
-    kernel while this thread polls an async batch posted to it: every poll
-    returns within 1 ms and at most 3 of the ~4 M over 100 us (round 5 held
-    the service's lock through the drain: polls waited the whole 300 ms; a
-    control thread that only reads the clock reports the host's own
-    scheduling gaps beside them), the stop really took the 300 ms, and the
-    batch comes back exact through the launch path.
+    kernel while this thread polls an async batch posted to it.  A control
+    thread that only reads the clock records the host's own descheduling
+    gaps over the same window; a slow poll (> 100 us) that overlaps one of
+    them is the host, not the library.  At most 3 of the millions of polls
+    may be slow with no such gap, none of them over 1 ms (round 5 held the
+    service's lock through the drain: polls waited the whole 300 ms).  The
+    stop really took the 300 ms, and the batch comes back exact through the
+    launch path.
     --slow-timeout: nobody stops it; the request gives up after 5 s (polls
     bounded the same way), re-runs exact on the launch path, and its line is
     quarantined until the kernel has left: a request meanwhile is launched,
