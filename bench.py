@@ -24,11 +24,17 @@ Also reported, on the same line:
                 config, two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
                 over the headline kernel in this run (traffic_live); else, or
                 if those fail, the committed summary under profiles/.
-  stream_read   the fastest plain streaming read of the same buffer we could
-                write (pcs_stream_read_dev, no hash): the practical read rate
-                of the part, within ~1 % of the hash kernels on 4 KiB pages
-                (profiles/r02/stream_sleep_lab.txt); context, not the roofline
-                peak (that is the 8 TB/s spec).
+  ceiling       the measured streaming-read ceiling: pcs_stream_read_dev
+                (the headline kernel's structure without the hash, at its
+                measured-best occupancy) and the hash kernel alternated under
+                one protocol; stream_read_GBps, and roofline.frac_of_ceiling =
+                achieved / that ceiling.
+  cold          the caller's exact protocol (W warmup + K timed steps) run at
+                process start, before the 1.5 s settle the headline uses.
+  host_inclusive (N = 1, default) pages starting in host memory, 1 GiB: pinned
+                hipMemcpyAsync H2D -> kernel -> D2H, gather, and a registered
+                zero-copy pool; GiB/s, fraction of PCIe Gen5 x16, digest parity
+                per leg, with cpu_ref_inmem_all_cores beside them.
   cpu_baseline  BASELINE config 1: the reference's own xxHash (oracle/_ref) on
                 ONE host thread, reading every page of a 1 GiB file of 4 KiB
                 pages and validating it like page_checksum_tool / page.cpp:25-31;

@@ -26,6 +26,8 @@
 //            spent inside the library's calls
 //   async_service  the same with the service on (Q lines per thread): a
 //            submit is a mailbox write instead of a kernel launch
+//   async_service_q1  one batch in flight per thread, so that eight threads
+//            fit the service's eight request lines and its gate stays open
 // Output per form and thread count: GiB/s checked, shard-thread CPU seconds
 // per GiB, and the CPU saved per GiB against the reference loop; then the
 // cores a GPU frees at its host-fed rate.  Verdict flips are checked: every
@@ -248,9 +250,9 @@ int main(int argc, char** argv) {
                     "in_call/GiB", "saved/GiB", "served", "bad");
         double ref_per_gib = 0;
         for (int T : {1, 8}) {
-            for (const char* form : {"ref", "sync", "service", "async", "async_service"}) {
-                const bool svc = std::strcmp(form, "service") == 0 || std::strcmp(form, "async_service") == 0;
-                const int Q = 4;
+            for (const char* form : {"ref", "sync", "service", "async", "async_service", "async_service_q1"}) {
+                const bool svc = std::strstr(form, "service") != nullptr;
+                const int Q = std::strcmp(form, "async_service_q1") == 0 ? 1 : 4;
                 // a line per request that can be in flight (at most 8 lines)
                 if (svc) StartChecksumService(std::strcmp(form, "service") == 0 ? 4 : 2, 1000,
                                               std::min(8, std::strcmp(form, "service") == 0 ? T : T * Q));
