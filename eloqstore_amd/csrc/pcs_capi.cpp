@@ -1154,9 +1154,6 @@ int batch_failed(pcs_batch* b, int rc) {
     return rc;
 }
 
-// Launch path of an asynchronous batch (arguments checked, n > 0): zero-copy
-// over registered pages, else staged (gather or direct DMA), on the batch's
-// own stream; completion is seen by poll / wait.
 // Result buffers of a batch: at least a service-sized batch (256 pages), so a
 // batch the service gives back never grows them from a poll (freeing device
 // or pinned memory synchronises the device: the poll would wait for every
@@ -1179,6 +1176,9 @@ int batch_results(pcs_batch* b, uint64_t n) {
     return PCS_OK;
 }
 
+// Launch path of an asynchronous batch (arguments checked, n > 0): zero-copy
+// over registered pages, else staged (gather or direct DMA), on the batch's
+// own stream; completion is seen by poll / wait.
 int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, uint64_t n, int algo) {
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != b->device) (void)hipSetDevice(b->device);
