@@ -168,6 +168,7 @@ TUNE_SERVICE_MAX_CALLERS = 28
 TUNE_SERVICE_REPOST_TEST = 30  # test only
 TUNE_ZC_STAMP_POLL_PAGES = 31
 TUNE_SERVICE_SLOW_EXIT_TEST = 33  # test only
+TUNE_ZC_BATCH_EVENT = 34
 
 # PCS_PATH_* bits (pcs_last_path / pcs_batch_path)
 PATH_SERVED = 1

@@ -1114,6 +1114,7 @@ struct pcs_batch {
     std::vector<uint8_t> svc_ok;
     std::vector<uint64_t> svc_dig;
     int path = 0;                      // PCS_PATH_* bits of the last submission (pcs_batch_path)
+    bool has_event = true;             // `done` was recorded behind the in-flight launch
 };
 
 namespace {
@@ -1216,7 +1217,12 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
         // result of a stamp batch)
         e = pcs::run_list(mode, algo, b->zc.d_ptrs, b->zc.h_ptrs, P, n, mode == PCS_BATCH_VALIDATE ? nullptr : b->zc.d_dig,
                           mode == PCS_BATCH_VALIDATE || b->zc_polled ? b->zc.d_ok : nullptr, s);
-        if (e == hipSuccess) e = hipEventRecord(b->done, s);
+        // A batch that completes from its landed verdicts / done bytes needs
+        // no event behind its kernel: its own stream answers the occasional
+        // "did the launch fail?" query (PCS_TUNE_ZC_BATCH_EVENT = 0, the
+        // default; one runtime call less per batch).
+        b->has_event = !b->zc_polled || pcs::get_tuning(PCS_TUNE_ZC_BATCH_EVENT) != 0;
+        if (e == hipSuccess && b->has_event) e = hipEventRecord(b->done, s);
         if (e != hipSuccess) return hip_fail(e, "pcs_batch_submit (zero-copy)");
         count(PCS_COUNTER_ZERO_COPY_LAUNCHES);
         b->state = 1;
@@ -1231,6 +1237,7 @@ int batch_launch(pcs_batch* b, int mode, const void* const* pages, uint64_t P, u
     if (e == hipSuccess)
         e = kmode ? hipMemcpyAsync(b->h_ok, b->d_ok, n, hipMemcpyDeviceToHost, s)
                   : hipMemcpyAsync(b->h_dig, b->d_dig, n * 8, hipMemcpyDeviceToHost, s);
+    b->has_event = true;
     if (e == hipSuccess) e = hipEventRecord(b->done, s);
     if (e != hipSuccess) return hip_fail(e, "pcs_batch_submit");
     b->state = 1;
@@ -1674,9 +1681,15 @@ int pcs_batch_poll(pcs_batch* b) {
         // call costs more than a scan of the verdict bytes).
         if (++b->zc_polls % kZcEventQueryPolls != 0) return 0;
     }
-    const hipError_t e = hipEventQuery(b->done);
+    const hipError_t e = b->has_event ? hipEventQuery(b->done) : hipStreamQuery(b->stream);
     if (e == hipErrorNotReady) return 0;
     if (e != hipSuccess) return batch_failed(b, hip_fail(e, "pcs_batch_poll"));
+    if (b->zc_polled) {  // the launch has finished: every verdict / done byte must be there now
+        b->zc_landed = verdicts_landed(b->zero_copy ? b->zc.h_ok : b->h_ok, b->zc_landed, b->n);
+        if (b->zc_landed != b->n)
+            return batch_failed(b, fail(PCS_ERR_HIP, "pcs_batch_poll: the launch finished without its results"));
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
     return batch_finalize(b);
 }
 

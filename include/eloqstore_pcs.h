@@ -92,7 +92,8 @@ enum pcs_flags {
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
  *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
  *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
- *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, pcs_thread_prepare (additive); pcs_stream_read_dev writes
+ *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, PCS_TUNE_ZC_BATCH_EVENT, pcs_thread_prepare (additive);
+ *      pcs_stream_read_dev writes
  *      one word per 4 KiB (was per 64 KiB: size d_out for the new count) */
 #define PCS_ABI_VERSION 6
 int pcs_abi_version(void);
@@ -369,6 +370,12 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     this many microseconds after deciding to
  *                                     leave (a stop or restart must not make
  *                                     pollers wait for them)
+ *   PCS_TUNE_ZC_BATCH_EVENT       [0] asynchronous zero-copy batches that
+ *                                     complete from their landed verdicts /
+ *                                     done bytes: 1 records an event behind
+ *                                     the kernel (round 5), 0 queries the
+ *                                     batch's stream instead (one runtime
+ *                                     call less per batch)
  * Keys 4, 5, 10, 12, 14, 16-22, 25, 29 and 32 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -397,6 +404,7 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_REPOST_TEST = 30,
     PCS_TUNE_ZC_STAMP_POLL_PAGES = 31,
     PCS_TUNE_SERVICE_SLOW_EXIT_TEST = 33,
+    PCS_TUNE_ZC_BATCH_EVENT = 34,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -202,17 +202,21 @@ def test_batch_skip_verify_and_failed_submit():
         b.close()
 
 
-@pytest.mark.parametrize("poll", [1, 0])
-def test_zero_copy_validate_completion_forms(poll):
+@pytest.mark.parametrize("poll,event", [(1, 0), (0, 0), (1, 1)])
+def test_zero_copy_validate_completion_forms(poll, event):
     """PCS_TUNE_ZC_POLL: a zero-copy validate completes when every verdict
     has landed in host memory (1, default) or on the launch's completion
-    signal (0).  Back-to-back sync calls and async batches, inline (<= 256
-    pages) and host-memory page lists, each call with a different corrupted
-    page, the pool rewritten between calls: every verdict and first-bad index
-    must match the oracle."""
+    signal (0).  PCS_TUNE_ZC_BATCH_EVENT: an async batch completing from its
+    verdicts has no event behind its kernel (0, default) or one (1).
+    Back-to-back sync calls and async batches, inline (<= 256 pages) and
+    host-memory page lists, each call with a different corrupted page, the
+    pool rewritten between calls: every verdict and first-bad index must
+    match the oracle."""
     P = 4096
     saved = pcs.get_tuning(pcs.TUNE_ZC_POLL)
+    saved_ev = pcs.get_tuning(pcs.TUNE_ZC_BATCH_EVENT)
     pcs.set_tuning(pcs.TUNE_ZC_POLL, poll)
+    pcs.set_tuning(pcs.TUNE_ZC_BATCH_EVENT, event)
     try:
         with pcs.PagePool(1024, P) as pool:
             pool.pages[:] = oracle.fill_pages(P, 1024, 0x2CC).reshape(1024, P)
@@ -243,6 +247,7 @@ def test_zero_copy_validate_completion_forms(poll):
                 b2.close()
     finally:
         pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
+        pcs.set_tuning(pcs.TUNE_ZC_BATCH_EVENT, saved_ev)
 
 
 @pytest.mark.parametrize("poll", [0, 1])
