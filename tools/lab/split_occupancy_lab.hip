@@ -73,9 +73,9 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_fill_lab, dim3(8192), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(pages), bytes / 8);
     CK(hipDeviceSynchronize());
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_split_capped<16384>),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, 160000));
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 150000));
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_split_capped<65536>),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, 160000));
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 150000));
     struct V {
         std::string name;
         uint64_t n, P;
