@@ -729,6 +729,12 @@ Service* current_service() {
 
 constexpr int kNotServed = 1;  // not eligible or declined: the caller takes the launch path
 constexpr int kFallback = 2;   // the service could not answer (stopped, no answer in time): launch path
+constexpr int kBusy = 3;       // the service's lock stayed held past kSubmitLockWait: launch path
+// A submit waits this long at most for the service's lock (held for a launch
+// of a new generation by another thread, which now and then takes
+// milliseconds inside the runtime: the soak's 1.2-6.1 ms submits, round 6),
+// then takes the launch path instead.
+constexpr auto kSubmitLockWait = std::chrono::microseconds(20);
 
 // PCS_TUNE_SERVICE_TEAR_TEST (test only): microseconds between posting seq
 // and writing the request words, so the kernel's polls see a new seq beside
@@ -872,16 +878,30 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
             k = c;
     }
     if (k < 0) return kNotServed;
-    std::unique_lock<std::mutex> lk(sv.mu);
-    if (sv.device < 0 || k >= sv.lines) {
+    // The line is ours: translate the page addresses into it and arm its
+    // verdict words before taking the lock (round 6: 256-page requests
+    // spent 0.4-0.6 ms in submit with both under the lock while other threads
+    // posted theirs).  No workgroup reads or writes a free line's words for
+    // a request: its last request was answered or given up (its kernel
+    // gone), and a waiting kernel only looks past them at a new seq, which
+    // is posted under the lock below.
+    pcs::ServiceLine* ln = sv.h ? &sv.h->line[k] : nullptr;
+    const int64_t tear_us = pcs::get_tuning(kTuneServiceTearTest);
+    uint64_t local[pcs::kServiceMaxPages];
+    if (!ln || !g_regions.translate(pages, n, P, tear_us > 0 ? local : ln->ptrs)) {
         sv.line[k].owner.store(0, std::memory_order_release);
         return kNotServed;
     }
-    pcs::ServiceLine* ln = &sv.h->line[k];
-    const int64_t tear_us = pcs::get_tuning(kTuneServiceTearTest);
-    uint64_t local[pcs::kServiceMaxPages];
-    uint64_t* dst = tear_us > 0 ? local : ln->ptrs;
-    if (!g_regions.translate(pages, n, P, dst)) {
+    for (uint64_t i = 0; i < n; ++i) ln->ok[i] = pcs::kServicePending;
+    std::unique_lock<std::mutex> lk(sv.mu, std::defer_lock);
+    for (const auto t0 = Service::clock::now(); !lk.try_lock();) {
+        if (Service::clock::now() - t0 > kSubmitLockWait) {
+            sv.line[k].owner.store(0, std::memory_order_release);
+            return kBusy;
+        }
+        __builtin_ia32_pause();
+    }
+    if (sv.device < 0 || k >= sv.lines) {
         sv.line[k].owner.store(0, std::memory_order_release);
         return kNotServed;
     }
@@ -891,7 +911,6 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
     r.k = k;
     r.n = n;
     r.stamp = stamp;
-    for (uint64_t i = 0; i < n; ++i) ln->ok[i] = pcs::kServicePending;
     if (!service_waiting(sv, k, Service::clock::now())) {
         if (int rc = service_launch_locked(sv)) {
             (void)service_retire_locked(sv, nullptr);  // nothing was posted: the line is free again
@@ -1038,7 +1057,8 @@ int service_run(Service* svp, const void* const* pages, uint64_t P, uint64_t n, 
                 uint64_t* first_bad) {
     ServiceReq r;
     const int s = service_submit(r, svp, pages, P, n, algo, ok == nullptr);
-    if (s != PCS_OK) return s;
+    if (s == kBusy) t_path |= PCS_PATH_LOCK_SKIPPED;
+    if (s != PCS_OK) return s == kBusy ? kNotServed : s;
     int p;
     while ((p = service_progress(r)) == 0) __builtin_ia32_pause();  // the sibling hyperthread may be a shard thread
     int rc = p == 1 ? service_collect(r, ok, first_bad) : p == kFallback ? kNotServed : p;
@@ -1651,6 +1671,7 @@ int pcs_batch_submit_ex(pcs_batch* b, int mode, const void* const* pages, uint64
                 return PCS_OK;
             }
             if (r < 0) return batch_failed(b, r);
+            if (r == kBusy) b->path |= PCS_PATH_LOCK_SKIPPED;
         }
     }
     if (int rc = batch_launch(b, mode, pages, P, n, algo)) return batch_failed(b, rc);

@@ -232,7 +232,8 @@ enum pcs_path {
     PCS_PATH_FALLBACK = 4,        /* posted to the service, then re-run on the launch path */
     PCS_PATH_REPOSTED = 8,        /* re-posted to a newer service generation at least once */
     PCS_PATH_NEW_GENERATION = 16, /* queued a new service kernel: none was certainly waiting */
-    PCS_PATH_LOCK_SKIPPED = 32,   /* a poll found the service's lock held and returned without it */
+    PCS_PATH_LOCK_SKIPPED = 32,   /* a poll found the service's lock held and returned without it, or a
+                                     submit gave up waiting for it (20 us) and took the launch path */
 };
 int pcs_last_path(void);
 int pcs_batch_path(const pcs_batch *b);
