@@ -87,6 +87,46 @@ __global__ __launch_bounds__(256) void k_read(const uint8_t* __restrict__ buf, u
     if (n == 0) pad[threadIdx.x] = 0;
 }
 
+// k_read with each 16-lane group reading TWO pages (32 dwordx4 loads per lane
+// in flight), 32 pages per workgroup; NT: non-temporal (1) or default policy
+template <int NPG, bool NT>
+__global__ __launch_bounds__(256) void k_read_multi(const uint8_t* __restrict__ buf, uint64_t n,
+                                                   uint64_t* __restrict__ out) {
+    extern __shared__ uint64_t pad[];
+    __shared__ uint64_t tile_h[16 * NPG];
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint64_t ntiles = (n + 16 * NPG - 1) / (16 * NPG);
+    const uint64_t t = xcd_tile(blockIdx.x, ntiles);
+    u32x4 d[NPG][16];
+#pragma unroll
+    for (int q = 0; q < NPG; ++q) {
+        const uint64_t pg = t * 16 * NPG + q * 16 + grp;
+        const u32x4* base = reinterpret_cast<const u32x4*>(buf + (pg < n ? pg : 0) * 4096ull) + g;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) d[q][c] = ld16<NT>(base + c * 16);
+    }
+#pragma unroll
+    for (int q = 0; q < NPG; ++q) {
+        uint32_t x = 0, y = 0, z = 0, v = 0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            x ^= d[q][c].x;
+            y += d[q][c].y;
+            z ^= d[q][c].z;
+            v += d[q][c].w;
+        }
+        uint64_t r = ((uint64_t)(x ^ z) << 32) | (y + v);
+        r ^= dpp64<kRowRor1>(r);
+        r ^= dpp64<kRowRor2>(r);
+        r ^= dpp64<kRowRor4>(r);
+        r ^= dpp64<kRowRor8>(r);
+        if (g == 0) tile_h[q * 16 + grp] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16 * NPG && t * 16 * NPG + threadIdx.x < n) st_nt(out + t * 16 * NPG + threadIdx.x, tile_h[threadIdx.x]);
+    if (n == 0) pad[threadIdx.x] = 0;
+}
+
 __global__ void k_fill(uint64_t* p, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t z = i + 0x9E3779B97F4A7C15ull;
@@ -111,6 +151,10 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hash), hipFuncAttributeMaxDynamicSharedMemorySize, 160000));
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_read), hipFuncAttributeMaxDynamicSharedMemorySize, 160000));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_read_multi<2, true>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 150000));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_read_multi<1, false>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 150000));
     struct V {
         std::string name;
         uint64_t n;
@@ -134,6 +178,23 @@ int main(int argc, char** argv) {
                           o ? std::to_string(o).c_str() : "7 (native)");
             const size_t lds = pad_for(o);
             vs.push_back({nm, n, false, [=] { hipLaunchKernelGGL(k_read, dim3(g), dim3(256), lds, 0, pages, n, out); }, {}});
+        }
+        for (int o : {1, 2, 3}) {  // two pages per group: twice the bytes in flight per wave
+            char nm[64];
+            std::snprintf(nm, sizeof nm, "%s read2 waves/SIMD %d", n == nbig ? "32 GiB" : " 4 GiB", o);
+            const size_t lds = pad_for(o);
+            const unsigned g2 = (unsigned)(n / 32);
+            vs.push_back({nm, n, false,
+                          [=] { hipLaunchKernelGGL((k_read_multi<2, true>), dim3(g2), dim3(256), lds, 0, pages, n, out); },
+                          {}});
+        }
+        for (int o : {2, 3}) {  // default cache policy
+            char nm[64];
+            std::snprintf(nm, sizeof nm, "%s read-cached waves/SIMD %d", n == nbig ? "32 GiB" : " 4 GiB", o);
+            const size_t lds = pad_for(o);
+            vs.push_back({nm, n, false,
+                          [=] { hipLaunchKernelGGL((k_read_multi<1, false>), dim3(g), dim3(256), lds, 0, pages, n, out); },
+                          {}});
         }
     }
     for (auto& v : vs) {  // every variant launches; hash digests equal the uncapped ones
