@@ -71,7 +71,7 @@ hipError_t run_stream_read(const uint8_t* buf, uint64_t bytes, uint64_t* out, hi
 // system-scope.  `gen` names the newest generation: a kernel of an older one
 // leaves at its next poll.
 constexpr int kServiceMaxPages = 256;
-constexpr int kServiceMaxLines = 32;  // round 6: 8 -> 32 (many async batches per GPU)
+constexpr int kServiceMaxLines = 8;
 constexpr int kServiceLineWords = 16;
 constexpr int kServiceCheckWord = 3;
 constexpr int kServiceLinePtrs = kServiceLineWords - 4;

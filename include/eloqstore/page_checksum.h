@@ -122,7 +122,7 @@ void UnregisterPagePool(void* base);
 // faster than the reference loop from 24 pages, both ways).  The kernel holds
 // `workgroups` CUs (16 serves 128-256 pages 10-15 % faster than 4) and
 // leaves after idle_us without a request or 2 * idle_us of life; the next
-// request starts a new one.  `lines` request lines (1-32) let that many calls
+// request starts a new one.  `lines` request lines (1-8) let that many calls
 // be served at once, each line by its own `workgroups` workgroups.  A call
 // that finds every line owned, or that arrives while more than
 // PCS_TUNE_SERVICE_MAX_CALLERS + lines - 1 eligible calls are in progress on

@@ -92,8 +92,7 @@ enum pcs_flags {
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
  *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
  *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
- *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, PCS_TUNE_ZC_BATCH_EVENT, pcs_thread_prepare, up to 32
- *      service request lines (was 8) (additive);
+ *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, PCS_TUNE_ZC_BATCH_EVENT, pcs_thread_prepare (additive);
  *      pcs_stream_read_dev writes
  *      one word per 4 KiB (was per 64 KiB: size d_out for the new count) */
 #define PCS_ABI_VERSION 6
@@ -263,7 +262,7 @@ int pcs_batch_path(const pcs_batch *b);
  * an idle_us out of range, or when the device's service is already running.
  * Services still running at exit are stopped by an atexit handler. */
 int pcs_service_start(int workgroups, uint32_t idle_us);
-/* The same with `lines` request lines (1 .. 32; 1 .. 8 before ABI 6), each served by its own
+/* The same with `lines` request lines (1 .. 8), each served by its own
  * `workgroups_per_line` workgroups (lines x workgroups_per_line <= 256): up
  * to `lines` calls on the device are in flight through the service at once,
  * each on a line of its own.  pcs_service_start(wg, idle) = _ex(1, wg, idle). */

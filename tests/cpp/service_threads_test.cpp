@@ -33,7 +33,7 @@
 // --soak SECONDS runs only the soak instead: eight threads mix sync
 // validates, async validates and stamps of their own pages (every validate
 // with a corrupted page, every stamp over a zeroed header) while a controller
-// thread keeps changing the service under them: stop, restart with 1-32 lines
+// thread keeps changing the service under them: stop, restart with 1-8 lines
 // of 1-4 workgroups and another idle time, gate knob 0/2/4, short torn-line
 // drills, and re-post drills (PCS_TUNE_SERVICE_REPOST_TEST: the next 1-4
 // requests are posted as a stale partial answer of an earlier generation,
@@ -605,7 +605,7 @@ int soak(char* pool, int T, double secs) {
                 std::this_thread::sleep_for(std::chrono::milliseconds(ms));
                 stopped_ms += ms;
             }
-            const int lines = 1 << (splitmix(rng) % 6), wpl = 1 << (splitmix(rng) % 3);
+            const int lines = 1 << (splitmix(rng) % 4), wpl = 1 << (splitmix(rng) % 3);
             const uint32_t idles[] = {0, 200, 500, 5000};
             CHECK(pcs_service_start_ex(lines, wpl, idles[splitmix(rng) % 4]) == PCS_OK);
             restart_epoch.fetch_add(1, std::memory_order_acq_rel);

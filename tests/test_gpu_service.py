@@ -668,7 +668,7 @@ def test_service_lifecycle():
     for bad in ((0, 0), (257, 0), (4, 100), (4, 2000000)):
         with pytest.raises(pcs.PcsError):
             pcs._call("pcs_service_start", *bad)
-    for bad in ((0, 1, 0), (33, 1, 0), (4, 65, 0), (2, 0, 0), (2, 2, 100)):
+    for bad in ((0, 1, 0), (9, 1, 0), (4, 65, 0), (2, 0, 0), (2, 2, 100)):
         with pytest.raises(pcs.PcsError):
             pcs._call("pcs_service_start_ex", *bad)
     with stamped_pool(64, P, 0x5EC) as pool:

@@ -260,7 +260,7 @@ int main(int argc, char** argv) {
                 const int Q = std::strcmp(form, "async_service_q1") == 0 ? 1 : 4;
                 // a line per request that can be in flight (at most 8 lines)
                 if (svc) StartChecksumService(std::strcmp(form, "service") == 0 ? 4 : 2, 1000,
-                                              std::min(32, std::strcmp(form, "service") == 0 ? T : T * Q));
+                                              std::min(8, std::strcmp(form, "service") == 0 ? T : T * Q));
                 Point pt = run(pool, form, T, Q, write, secs, work_unit);
                 if (svc) StopChecksumService();
                 pt.path = svc ? "service" : std::strcmp(form, "ref") == 0 ? "cpu" : "zero-copy launch";
