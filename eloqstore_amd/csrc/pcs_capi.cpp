@@ -188,19 +188,53 @@ uint64_t verdicts_landed(const uint8_t* h_ok, uint64_t from, uint64_t n) {
     while (from < n && v[from] != kVerdictPending) ++from;
     return from;
 }
-// Spin until every verdict has landed; the stream is queried every 4096
-// spins so a failed or finished launch that wrote no verdict cannot hang the
-// caller (then the stream's own status decides).
+// A synchronous caller's wait between checks: spin (pause) for the first
+// PCS_TUNE_SYNC_SPIN_US microseconds of the call, then sleep ~10 µs per
+// check (0, the default: spin throughout).  A spinning caller costs its core
+// for the whole wait; once several shard threads share the GPU's PCIe link
+// the sync calls cost as much CPU as the loop they replace,
+// and sleeping gives that time to other threads at some latency.
+class SyncWaiter {
+public:
+    SyncWaiter() : spin_us_(pcs::get_tuning(PCS_TUNE_SYNC_SPIN_US)) {
+        if (spin_us_ > 0) t0_ = std::chrono::steady_clock::now();
+    }
+    // one wait between two checks; true once the caller sleeps
+    bool pause() {
+        if (spin_us_ <= 0 || (!sleeping_ && (++n_ & 63) != 0)) {
+            __builtin_ia32_pause();  // spin politely: the sibling hyperthread may be a shard thread
+            return false;
+        }
+        if (!sleeping_ && std::chrono::steady_clock::now() - t0_ < std::chrono::microseconds(spin_us_)) {
+            __builtin_ia32_pause();
+            return false;
+        }
+        sleeping_ = true;
+        std::this_thread::sleep_for(std::chrono::microseconds(10));
+        return true;
+    }
+
+private:
+    int64_t spin_us_;
+    std::chrono::steady_clock::time_point t0_{};
+    uint32_t n_ = 0;
+    bool sleeping_ = false;
+};
+
+// Wait until every verdict has landed; the stream is queried every 4096
+// spins (every 16 sleeps) so a failed or finished launch that wrote no
+// verdict cannot hang the caller (then the stream's own status decides).
 hipError_t wait_verdicts(const uint8_t* h_ok, uint64_t n, hipStream_t s) {
     uint64_t at = 0;
-    for (uint32_t spin = 0;; ++spin) {
+    SyncWaiter w;
+    for (uint32_t spin = 0, naps = 0;; ++spin) {
         at = verdicts_landed(h_ok, at, n);
         if (at == n) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return hipSuccess;
         }
-        __builtin_ia32_pause();  // spin politely: the sibling hyperthread may be a shard thread
-        if ((spin & 4095) == 4095) {
+        const bool slept = w.pause();
+        if ((spin & 4095) == 4095 || (slept && (++naps & 15) == 0)) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {  // finished: every verdict must be there now
                 at = verdicts_landed(h_ok, at, n);
@@ -1060,7 +1094,8 @@ int service_run(Service* svp, const void* const* pages, uint64_t P, uint64_t n, 
     if (s == kBusy) t_path |= PCS_PATH_LOCK_SKIPPED;
     if (s != PCS_OK) return s == kBusy ? kNotServed : s;
     int p;
-    while ((p = service_progress(r)) == 0) __builtin_ia32_pause();  // the sibling hyperthread may be a shard thread
+    SyncWaiter w;
+    while ((p = service_progress(r)) == 0) w.pause();
     int rc = p == 1 ? service_collect(r, ok, first_bad) : p == kFallback ? kNotServed : p;
     if (p == kFallback) r.path |= PCS_PATH_FALLBACK;
     t_path = r.path;

@@ -1430,7 +1430,7 @@ uint64_t next_call_id() {
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 35;
+constexpr int kTuneKeys = 36;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1448,7 +1448,7 @@ constexpr int kTuneKeys = 35;
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
                                       false, true,  false, false, false, true,  false, false, true,  false,
-                                      false};
+                                      false, false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4/5 -> 1/2/4/3)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1474,7 +1474,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*zero-copy XXH3 stamps: done-byte completion up to this many pages*/ 256,
                                           /*retired (round 5 lab: service polls in flight)*/ 0,
                                           /*test only: service kernels serve nothing and leave this many us late*/ 0,
-                                          /*zero-copy batches completing from their verdicts: event behind the kernel*/ 0};
+                                          /*zero-copy batches completing from their verdicts: event behind the kernel*/ 0,
+                                          /*sync host calls: microseconds of spinning before sleeping between checks (0 = spin)*/ 0};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;

@@ -92,7 +92,8 @@ enum pcs_flags {
  *   5  round 5: PCS_TUNE_SERVICE_REPOST_TEST, PCS_TUNE_ZC_STAMP_POLL_PAGES,
  *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
  *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
- *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, PCS_TUNE_ZC_BATCH_EVENT, pcs_thread_prepare (additive);
+ *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, PCS_TUNE_ZC_BATCH_EVENT, PCS_TUNE_SYNC_SPIN_US,
+ *      pcs_thread_prepare (additive);
  *      pcs_stream_read_dev writes
  *      one word per 4 KiB (was per 64 KiB: size d_out for the new count) */
 #define PCS_ABI_VERSION 6
@@ -377,6 +378,13 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     the kernel (round 5), 0 queries the
  *                                     batch's stream instead (one runtime
  *                                     call less per batch)
+ *   PCS_TUNE_SYNC_SPIN_US         [0] synchronous host calls (validate, stamp,
+ *                                     pcs_batch_wait) spin on their results
+ *                                     for this many microseconds, then sleep
+ *                                     ~10 µs between checks; 0 = spin
+ *                                     throughout (lowest latency; a loaded
+ *                                     store's sync callers then burn their
+ *                                     cores)
  * Keys 4, 5, 10, 12, 14, 16-22, 25, 29 and 32 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -406,6 +414,7 @@ enum pcs_tune_key {
     PCS_TUNE_ZC_STAMP_POLL_PAGES = 31,
     PCS_TUNE_SERVICE_SLOW_EXIT_TEST = 33,
     PCS_TUNE_ZC_BATCH_EVENT = 34,
+    PCS_TUNE_SYNC_SPIN_US = 35,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

@@ -202,12 +202,14 @@ def test_batch_skip_verify_and_failed_submit():
         b.close()
 
 
-@pytest.mark.parametrize("poll,event", [(1, 0), (0, 0), (1, 1)])
-def test_zero_copy_validate_completion_forms(poll, event):
+@pytest.mark.parametrize("poll,event,spin", [(1, 0, 0), (0, 0, 0), (1, 1, 0), (1, 0, 1)])
+def test_zero_copy_validate_completion_forms(poll, event, spin):
     """PCS_TUNE_ZC_POLL: a zero-copy validate completes when every verdict
     has landed in host memory (1, default) or on the launch's completion
     signal (0).  PCS_TUNE_ZC_BATCH_EVENT: an async batch completing from its
     verdicts has no event behind its kernel (0, default) or one (1).
+    PCS_TUNE_SYNC_SPIN_US: sync callers spin throughout (0, default) or sleep
+    between checks after 1 us (every wait of this test then sleeps).
     Back-to-back sync calls and async batches, inline (<= 256 pages) and
     host-memory page lists, each call with a different corrupted page, the
     pool rewritten between calls: every verdict and first-bad index must
@@ -215,8 +217,10 @@ def test_zero_copy_validate_completion_forms(poll, event):
     P = 4096
     saved = pcs.get_tuning(pcs.TUNE_ZC_POLL)
     saved_ev = pcs.get_tuning(pcs.TUNE_ZC_BATCH_EVENT)
+    saved_spin = pcs.get_tuning(pcs.TUNE_SYNC_SPIN_US)
     pcs.set_tuning(pcs.TUNE_ZC_POLL, poll)
     pcs.set_tuning(pcs.TUNE_ZC_BATCH_EVENT, event)
+    pcs.set_tuning(pcs.TUNE_SYNC_SPIN_US, spin)
     try:
         with pcs.PagePool(1024, P) as pool:
             pool.pages[:] = oracle.fill_pages(P, 1024, 0x2CC).reshape(1024, P)
@@ -248,6 +252,7 @@ def test_zero_copy_validate_completion_forms(poll, event):
     finally:
         pcs.set_tuning(pcs.TUNE_ZC_POLL, saved)
         pcs.set_tuning(pcs.TUNE_ZC_BATCH_EVENT, saved_ev)
+        pcs.set_tuning(pcs.TUNE_SYNC_SPIN_US, saved_spin)
 
 
 @pytest.mark.parametrize("poll", [0, 1])

@@ -30,6 +30,8 @@
 //            fit the service's eight request lines and its gate stays open
 //   async_event  async with PCS_TUNE_ZC_BATCH_EVENT = 1 (round 5's event
 //            recorded behind every zero-copy batch's kernel)
+//   sync_sleep  sync with PCS_TUNE_SYNC_SPIN_US = 30: the caller spins 30 us,
+//            then sleeps ~10 us between checks
 // Output per form and thread count: GiB/s checked, shard-thread CPU seconds
 // per GiB, and the CPU saved per GiB against the reference loop; then the
 // cores a GPU frees at its host-fed rate.  Verdict flips are checked: every
@@ -147,7 +149,7 @@ Point run(const std::vector<char*>& pool, const std::string& form, int T, int Q,
                     }
                     done += kBatch;
                 }
-            } else if (form == "sync" || form == "service") {
+            } else if (form == "sync" || form == "service" || form == "sync_sleep") {
                 while (Clock::now() < stop) {
                     pick(ptrs[0]);
                     if (write) {
@@ -252,11 +254,12 @@ int main(int argc, char** argv) {
                     "in_call/GiB", "saved/GiB", "served", "bad");
         double ref_per_gib = 0;
         for (int T : {1, 8}) {
-            for (const char* form : {"ref", "sync", "service", "async", "async_event", "async_service",
+            for (const char* form : {"ref", "sync", "sync_sleep", "service", "async", "async_event", "async_service",
                                      "async_service_q1"}) {
                 const bool svc = std::strstr(form, "service") != nullptr;
                 const bool ev = std::strcmp(form, "async_event") == 0;
                 pcs_set_tuning(PCS_TUNE_ZC_BATCH_EVENT, ev ? 1 : 0);
+                pcs_set_tuning(PCS_TUNE_SYNC_SPIN_US, std::strcmp(form, "sync_sleep") == 0 ? 30 : 0);
                 const int Q = std::strcmp(form, "async_service_q1") == 0 ? 1 : 4;
                 // a line per request that can be in flight (at most 8 lines)
                 if (svc) StartChecksumService(std::strcmp(form, "service") == 0 ? 4 : 2, 1000,
