@@ -174,10 +174,79 @@ static void test_concurrent() {
                 (unsigned long long)miss.load(), (unsigned long long)bad.load());
 }
 
+// Round 6 replaced the registry's std::map with a sorted array and a
+// branchless binary search: random non-overlapping regions (sub-page to
+// multi-MiB, some adjacent), random adds and removes, and random page
+// queries (inside, straddling an end, in gaps, before the first and after the
+// last region) must agree with a brute-force scan on every translate and run.
+static void test_random_against_brute_force() {
+    uint64_t s = 0x5EED;
+    auto rnd = [&s] {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    struct R {
+        uintptr_t base;
+        uint64_t bytes;
+        uintptr_t dev;
+    };
+    for (int round = 0; round < 40; ++round) {
+        RegionRegistry r;
+        std::vector<R> live;
+        uintptr_t at = 0x100000 + (rnd() % 64) * 16;
+        for (int i = 0; i < 300; ++i) {
+            const uint64_t bytes = 16 * (1 + rnd() % (rnd() % 4 ? 64 : 65536));
+            if (rnd() % 3) at += 16 * (rnd() % 4096);  // a gap, or adjacent
+            const uintptr_t dev = 0x7000000000ull + rnd() % (1ull << 32) * 16;
+            CHECK(r.add(at, bytes, dev, false) == RegionRegistry::kOk);
+            live.push_back({at, bytes, dev});
+            at += bytes;
+        }
+        for (int i = 0; i < 60; ++i) {  // remove some
+            const size_t k = rnd() % live.size();
+            CHECK(r.remove(live[k].base, false) == RegionRegistry::kOk);
+            live.erase(live.begin() + k);
+        }
+        CHECK(r.size() == live.size());
+        const uintptr_t lo = live.front().base - 4096, hi = at + 4096;
+        for (int q = 0; q < 3000; ++q) {
+            const uintptr_t a = (lo + rnd() % (hi - lo)) & ~uintptr_t(15);
+            const uint64_t P = 16 * (1 + rnd() % 16);
+            const R* hit = nullptr;
+            for (const R& x : live)
+                if (a >= x.base && a - x.base < x.bytes) hit = &x;
+            const bool want = hit && P <= hit->bytes - (a - hit->base);
+            const void* page[1] = {reinterpret_cast<const void*>(a)};
+            uint64_t dev = 0;
+            CHECK(r.translate(page, 1, P, &dev) == want);
+            if (want) CHECK(dev == hit->dev + (a - hit->base));
+            const RegionRegistry::Run run = r.run(a, a + P - 1);
+            CHECK(run == (!hit ? RegionRegistry::kNotRegistered : want ? RegionRegistry::kInside : RegionRegistry::kPastEnd));
+        }
+        // a batch across many regions, then one page outside fails the batch
+        std::vector<const void*> batch;
+        std::vector<uint64_t> want;
+        for (int i = 0; i < 128; ++i) {
+            const R& x = live[rnd() % live.size()];
+            const uintptr_t a = x.base + 16 * (rnd() % (x.bytes / 16));
+            batch.push_back(reinterpret_cast<const void*>(a));
+            want.push_back(x.dev + (a - x.base));
+        }
+        std::vector<uint64_t> got(batch.size());
+        CHECK(r.translate(batch.data(), batch.size(), 16, got.data()) && got == want);
+        batch[77] = reinterpret_cast<const void*>(hi + 4096);
+        CHECK(!r.translate(batch.data(), batch.size(), 16, got.data()));
+    }
+}
+
 int main() {
     test_add_remove();
     test_translate();
     test_concurrent();
+    test_random_against_brute_force();
     if (g_fail) {
         std::fprintf(stderr, "%d check(s) failed\n", g_fail);
         return 1;
