@@ -14,9 +14,10 @@ TAG=${1:-r02}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# (host-inclusive legs off: PCIe-bound, measured in the bench line itself)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o bench --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --no-live-traffic > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
-SHORT="--steps 5 --warmup 2 --sweep-steps 5 --sweep-warmup 1 --no-cpu-baseline --no-live-traffic"
+    python3 bench.py --no-cpu-baseline --no-live-traffic --no-host-inclusive > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
+SHORT="--steps 5 --warmup 2 --sweep-steps 5 --sweep-warmup 1 --no-cpu-baseline --no-live-traffic --no-host-inclusive"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- \
     python3 bench.py $SHORT > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- \

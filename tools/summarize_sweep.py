@@ -108,12 +108,22 @@ def main():
     for e in bench.get("sweep") or []:
         wanted.append({"key": e["key"], "steps": e["steps"], "frac": e["frac"], "avg_launch_ms": e["avg_launch_ms"],
                        "alg": e["algorithmic_bytes_per_launch"]})
+    # Round 6 bench phases: the `cold` run (W + K launches) precedes the
+    # headline's settle + warmup + timed segment, and the ceiling A/B
+    # (k_stream_read beside the hash kernel) follows it.  The headline takes
+    # the first segment with settle + K launches of a kernel; segments that
+    # hold k_stream_read are skipped.
+    settle_steps = (bench.get("settle") or {}).get("steps", 0) if bench.get("cold") else 0
     entries, si = [], 0
     for w in wanted:
         ks = []
+        need = w["steps"] + (settle_steps if w["key"] == "headline" else 0)
         while si < len(segs):
-            ks = seg_kernels(segs[si], w["steps"])
+            seg = segs[si]
             si += 1
+            if any("k_stream_read" in kname(r) for r in seg):
+                continue
+            ks = seg_kernels(seg, need)
             if ks:
                 break
         if not ks:
