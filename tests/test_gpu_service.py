@@ -814,3 +814,31 @@ def test_thread_prepare():
         th.start()
         th.join()
         assert not errors, errors
+
+
+def test_service_with_sleeping_sync_waits(service):
+    """PCS_TUNE_SYNC_SPIN_US = 1: a synchronous call through the service spins
+    1 us, then sleeps between checks.  Validates with a
+    corrupted page and stamps of 1-256 pages stay exact and served."""
+    P = 4096
+    saved = pcs.get_tuning(pcs.TUNE_SYNC_SPIN_US)
+    pcs.set_tuning(pcs.TUNE_SYNC_SPIN_US, 1)
+    try:
+        with stamped_pool(512, P, 0x5FD) as pool:
+            rng = np.random.default_rng(9)
+            for n in (1, 7, 64, 256):
+                idx = rng.permutation(512)[:n]
+                k = int(rng.integers(n))
+                pool.pages[idx[k], 2000] ^= 0x04
+                s0 = pcs.counter(SVC)
+                ok, fb = pcs.validate_ptrs(pool.ptr(idx), P)
+                pool.pages[idx[k], 2000] ^= 0x04
+                assert fb == k and ok.sum() == n - 1 and pcs.counter(SVC) == s0 + 1, n
+                assert pcs.lib().pcs_last_path() & pcs.PATH_SERVED
+            idx = np.arange(400, 500)
+            pool.pages[idx, :8] = 0
+            pcs.stamp_ptrs(pool.ptr(idx), P)
+            want = oracle.pages_digest(pool.pages[idx].reshape(-1), P, 0)
+            assert np.array_equal(pool.pages[idx, :8].copy().view(np.uint64).ravel(), want)
+    finally:
+        pcs.set_tuning(pcs.TUNE_SYNC_SPIN_US, saved)
