@@ -457,7 +457,7 @@ int slow_stop(char* pool) {
     CHECK(poll_ms >= 0.8 * kExitUs / 1000);  // ... and the batch was polled all that time
     CHECK((path & PCS_PATH_FALLBACK) && (path & PCS_PATH_LAUNCHED) && !(path & PCS_PATH_SERVED));
     check_result(b, v, 21);
-    CHECK(st.fallback_us < 2000.0);
+    CHECK(st.fallback_us < 20000.0);  // one launch (11-65 us; rare runtime stalls of 1-6 ms), not the kernel's exit
     pcs_batch_destroy(b);
     return poll_bound(st);
 }
@@ -490,7 +490,7 @@ int slow_timeout(char* pool) {
     std::fflush(stdout);
     check_result(b, v, 44);
     CHECK((path & PCS_PATH_FALLBACK) && !(path & PCS_PATH_SERVED) && !(path & PCS_PATH_REPOSTED));
-    CHECK(st.fallback_us < 2000.0);
+    CHECK(st.fallback_us < 20000.0);  // one launch (11-65 us; rare runtime stalls of 1-6 ms), not the kernel's exit
     CHECK(gave_up_s >= 4.9 && gave_up_s < 6.0);
     const int bound = poll_bound(st);
     // the line is quarantined until the slow kernel has left (~6 s after the
