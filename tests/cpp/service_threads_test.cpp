@@ -444,7 +444,7 @@ int slow_stop(char* pool) {
     const int path = pcs_batch_path(b);
     std::printf("slow stop: pcs_service_stop rc %d in %.1f ms (kernel exit delay %lld ms); batch done after %.1f ms "
                 "of polls: %llu polls, max %.1f us (slowest: %s), %llu over 100 us (the re-launching poll: %.1f us); "
-                "control thread: max gap %.1f us, %llu gaps over 100 us; slow polls no control gap explains: %llu "
+                "control thread: max gap %.1f us, %llu gaps over 100 us; slow polls that are the library's: %llu "
                 "(max %.1f us); path %s\n",
                 stop_rc.load(), stop_ms.load(), (long long)kExitUs / 1000, poll_ms, (unsigned long long)st.polls,
                 st.max_us, top_polls(st).c_str(), (unsigned long long)st.over, st.fallback_us, st.control_max_us,
@@ -481,7 +481,7 @@ int slow_timeout(char* pool) {
     const double gave_up_s = std::chrono::duration<double>(Clock::now() - p0).count();
     const int path = pcs_batch_path(b);
     std::printf("slow timeout: gave up after %.2f s: %llu polls, max %.1f us (slowest: %s), %llu over 100 us, "
-                "re-launching poll %.1f us, control thread max gap %.1f us (%llu over 100 us), unexplained slow polls "
+                "re-launching poll %.1f us, control thread max gap %.1f us (%llu over 100 us), slow polls that are the library's "
                 "%llu (max %.1f us), path %s\n", gave_up_s,
                 (unsigned long long)st.polls, st.max_us, top_polls(st).c_str(), (unsigned long long)st.over,
                 st.fallback_us, st.control_max_us, (unsigned long long)st.control_over,
