@@ -170,6 +170,7 @@ TUNE_ZC_STAMP_POLL_PAGES = 31
 TUNE_SERVICE_SLOW_EXIT_TEST = 33  # test only
 TUNE_ZC_BATCH_EVENT = 34
 TUNE_SYNC_SPIN_US = 35
+TUNE_SERVICE_DEPARTURE = 36
 
 # PCS_PATH_* bits (pcs_last_path / pcs_batch_path)
 PATH_SERVED = 1

@@ -86,10 +86,14 @@ struct ServiceLine {
     alignas(64) uint32_t ok[kServiceMaxPages];
     alignas(64) uint64_t torn_seq;    // kernel: the last seq it saw beside words that failed the check
 };
+constexpr int kServiceMaxWorkgroups = 256;  // lines * workgroups per line
 struct ServiceBox {
     alignas(64) uint64_t stop;  // host: 1 ends every waiting kernel
     uint64_t gen;               // host: the newest generation (written before its kernel is queued)
     ServiceLine line[kServiceMaxLines];
+    // kernel: departed[w] = the generation of the last workgroup w to leave,
+    // stored after every verdict / header store of it is visible system-wide
+    alignas(64) uint32_t departed[kServiceMaxWorkgroups];
 };
 static_assert(offsetof(ServiceLine, ptrs) == 4 * sizeof(uint64_t), "line words: seq, n, page_size, check, ptrs");
 static_assert(offsetof(ServiceBox, gen) == offsetof(ServiceBox, stop) + 8, "stop and gen are one poll's two words");
@@ -108,8 +112,9 @@ __host__ __device__ inline uint64_t service_word_mix(uint64_t w, uint64_t i) {
 // workgroup w serving line w / wpl.  Each serves its line's requests of that
 // generation until idle_ticks pass without one or, between requests, it has
 // lived life_ticks (both on the 100 MHz real-time clock), or stop is set, or
-// the box names a newer generation.  exit_ticks: test only (a kernel that
-// serves nothing and leaves that many ticks late; 0 in production).
+// the box names a newer generation; then it stores gen into departed[w].
+// exit_ticks: test only (a kernel that serves nothing and leaves that many
+// ticks late; 0 in production).
 hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                        uint64_t exit_ticks, hipStream_t s);
 

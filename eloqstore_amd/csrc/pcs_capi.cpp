@@ -610,6 +610,7 @@ struct Service {
     hipStream_t stream = nullptr;  // kept across restarts; recreated only when its kind changes
     int64_t stream_kind = -1;      // PCS_TUNE_SERVICE_STREAM it was created with
     hipEvent_t done[kServiceEvents] = {};  // done[g % 16]: recorded behind generation g's kernel
+    uint64_t slot_gen[kServiceEvents] = {};  // g << 1 | 1 queued a kernel of g, | 0 retired g (none)
     pcs::ServiceBox* h = nullptr;  // pinned, coherent, device-mapped; never freed
     pcs::ServiceBox* d = nullptr;  // its device alias
     std::atomic<uint32_t> gen{0};  // generation of the newest queued kernel (never reset; read unlocked)
@@ -654,18 +655,33 @@ int service_launch_locked(Service& sv) {
     hipError_t e = pcs::run_service(sv.d, sv.lines, sv.wpl, g, (uint64_t)sv.idle_us * 100,
                                     (uint64_t)sv.idle_us * 200, exit_ticks, sv.stream);
     if (e == hipSuccess) e = hipEventRecord(sv.done[g % kServiceEvents], sv.stream);
+    sv.slot_gen[g % kServiceEvents] = (uint64_t)g << 1 | 1;
     return finish(e, "service kernel launch");
+}
+
+// Have line k's workgroups of generation `gen` (wpl per line) all left?
+// Each stores its generation into its departure word after its last verdict
+// or header store is visible (k_service); a later generation's word in the
+// same slot says so too, since kernels on the service's one stream run in
+// order.  PCS_TUNE_SERVICE_DEPARTURE = 0: never consulted.
+bool departure_words() { return pcs::get_tuning(PCS_TUNE_SERVICE_DEPARTURE) != 0; }
+bool line_departed(const Service& sv, int k, int wpl, uint32_t gen) {
+    const volatile uint32_t* d = sv.h->departed + k * wpl;
+    for (int w = 0; w < wpl; ++w)
+        if ((int32_t)(d[w] - gen) < 0) return false;
+    return true;
 }
 
 // Line k's workgroups certainly still wait: launched less than life - margin
 // ago and the line last answered less than idle - margin ago (host time
-// bounds the kernel's clocks).
+// bounds the kernel's clocks), and none of them has said it left.
 bool service_waiting(const Service& sv, int k, Service::clock::time_point now) {
     const auto margin = std::chrono::microseconds(sv.idle_us / 4);
     const Service::clock::time_point answered{
         Service::clock::duration(sv.line[k].answered.load(std::memory_order_relaxed))};
     return sv.live && now - sv.launched < std::chrono::microseconds(2 * (uint64_t)sv.idle_us) - margin &&
-           now - answered < std::chrono::microseconds(sv.idle_us) - margin;
+           now - answered < std::chrono::microseconds(sv.idle_us) - margin &&
+           !(departure_words() && line_departed(sv, k, sv.wpl, sv.gen.load(std::memory_order_relaxed)));
 }
 
 // The check word of line `ln`'s request words as they now stand, with `seq`
@@ -712,6 +728,7 @@ uint32_t service_retire_locked(Service& sv, hipError_t* err) {
     sv.gen.store(g, std::memory_order_release);
     sv.live = false;
     const hipError_t e = hipEventRecord(sv.done[g % kServiceEvents], sv.stream);
+    sv.slot_gen[g % kServiceEvents] = (uint64_t)g << 1;
     if (err) *err = e;
     return g;
 }
@@ -845,6 +862,7 @@ struct ServiceReq {
     int k = 0;              // its line
     uint64_t n = 0, landed = 0, seq = 0;
     uint32_t gen = 0;       // the generation it is posted to
+    int wpl = 0;            // that generation's workgroups per line
     bool stamp = false;
     int relaunched = 0;
     uint32_t checked_gen = 0;  // the service's generation at the last check
@@ -881,10 +899,13 @@ thread_local int t_line_hint = -1;  // the line this thread used last: its first
 // header never written).  A host that re-posted without re-arming would
 // collect those as answers.  Needs gen >= 2 (generation gen - 1 then had a
 // kernel and its event); otherwise the request is posted normally and the
-// knob is not consumed.
+// knob is not consumed.  So is a generation gen - 1 that queued no kernel
+// (the one a stop or give-up retired): no workgroup of it could have
+// answered part of a request.
 constexpr int kTuneServiceRepostTest = PCS_TUNE_SERVICE_REPOST_TEST;
-uint32_t repost_drill(pcs::ServiceLine* ln, uint64_t n, bool stamp, uint32_t gen) {
-    if (gen < 2 || pcs::get_tuning(kTuneServiceRepostTest) <= 0 || !pcs::take_tuning(kTuneServiceRepostTest))
+uint32_t repost_drill(const Service& sv, pcs::ServiceLine* ln, uint64_t n, bool stamp, uint32_t gen) {
+    if (gen < 2 || sv.slot_gen[(gen - 1) % kServiceEvents] != ((uint64_t)(gen - 1) << 1 | 1) ||
+        pcs::get_tuning(kTuneServiceRepostTest) <= 0 || !pcs::take_tuning(kTuneServiceRepostTest))
         return gen;
     for (uint64_t i = 16; i < n; ++i) ln->ok[i] = stamp ? 1u : 0u;
     return gen - 1;
@@ -972,9 +993,10 @@ int service_submit(ServiceReq& r, Service* svp, const void* const* pages, uint64
     } else {
         ln->n = n;
         ln->page_size = page_word;
-        r.gen = repost_drill(ln, n, stamp, sv.gen.load(std::memory_order_relaxed));
+        r.gen = repost_drill(sv, ln, n, stamp, sv.gen.load(std::memory_order_relaxed));
         r.seq = service_post_locked(sv, k, r.gen);
     }
+    r.wpl = sv.wpl;
     r.posted = r.checked = Service::clock::now();
     r.checked_gen = r.gen;
     return PCS_OK;
@@ -992,12 +1014,19 @@ int service_progress(ServiceReq& r) {
         std::atomic_thread_fence(std::memory_order_acquire);
         return 1;
     }
-    // The kernel's state is checked every 50 µs, and at once when a newer
-    // generation has been started since the last check (this request must
-    // then be re-posted as soon as its own generation's kernel has left).
+    // Has the request's generation left its line?  With departure words the
+    // line's own words say so (re-post at once), and the runtime is asked
+    // about the kernel every 1 ms, for a failed kernel and the 5 s give-up.
+    // Without them the runtime is asked every 50 µs, and at once when a
+    // newer generation has been started since the last check (this request
+    // must then be re-posted as soon as its own generation's kernel has left).
     const auto now = Service::clock::now();
     const uint32_t g_now = sv.gen.load(std::memory_order_acquire);
-    if (now - r.checked < std::chrono::microseconds(50) && g_now == r.checked_gen) return 0;
+    const bool departure = departure_words();
+    const bool gone = departure && line_departed(sv, r.k, r.wpl, r.gen);
+    if (!gone && (departure ? now - r.checked < std::chrono::milliseconds(1)
+                            : now - r.checked < std::chrono::microseconds(50) && g_now == r.checked_gen))
+        return 0;
     r.checked = now;
     r.checked_gen = g_now;
     // Never wait for the lock: its holder (another thread's submit, start,
@@ -1012,7 +1041,7 @@ int service_progress(ServiceReq& r) {
     // event; a newer generation's event in the same ring slot is later on
     // the stream, so its completion implies this one's.)
     const hipError_t q = hipEventQuery(sv.done[r.gen % kServiceEvents]);
-    if (q == hipErrorNotReady) {
+    if (q == hipErrorNotReady && !gone) {
         if (now - r.posted < std::chrono::seconds(5)) return 0;
         // no answer in 5 s (a latency problem, not a failure): retire the
         // kernels and give the line up only once this one has left
@@ -1020,12 +1049,14 @@ int service_progress(ServiceReq& r) {
         r.quarantine = true;
         return kFallback;
     }
-    if (q != hipSuccess) {
+    if (q != hipSuccess && q != hipErrorNotReady) {
         (void)service_retire_locked(sv, nullptr);
         r.quarantine = true;
         return hip_fail(q, "service stream");
     }
-    // That kernel has left and this request is not fully answered (its
+    std::atomic_thread_fence(std::memory_order_acquire);  // after the departure words
+    // That kernel has left (or its workgroups on this line have, which is
+    // all that can write the line) and this request is not fully answered (its
     // workgroups reached a limit just before the post, a newer generation
     // replaced it, or the service was stopped): no workgroup can write this
     // line any more, and verdicts are idempotent, so the request is posted
@@ -1055,6 +1086,7 @@ int service_progress(ServiceReq& r) {
     g_reposts.fetch_add(1, std::memory_order_relaxed);
     r.path |= PCS_PATH_REPOSTED;
     r.gen = sv.gen.load(std::memory_order_relaxed);
+    r.wpl = sv.wpl;
     r.seq = service_post_locked(sv, r.k, r.gen);
     r.posted = Service::clock::now();
     return 0;

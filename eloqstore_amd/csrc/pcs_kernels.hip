@@ -1430,7 +1430,7 @@ uint64_t next_call_id() {
 // tuning knobs (pcs_set_tuning): read at every launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kTuneKeys = 36;
+constexpr int kTuneKeys = 37;
 // Keys retired in round 2 with the variants they selected (measured slower,
 // DESIGN.md §4): 4 XXH64 nt loads, 5 in-place stamp width, 10 descriptor tile
 // sort, 12 descriptor slices, 14 XXH64 descriptor sort; round-2 experiments
@@ -1448,7 +1448,7 @@ constexpr int kTuneKeys = 36;
 constexpr bool kRetired[kTuneKeys] = {false, false, false, false, true, true, false, false, false, false, true,  false,
                                       true,  false, true,  false, true,  true,  true,  true,  true,  true,  true,  false,
                                       false, true,  false, false, false, true,  false, false, true,  false,
-                                      false, false};
+                                      false, false, false};
 std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 blocks/CU*/ 0, /*xxh3 nt*/ 1,
                                           /*retired*/ 0, /*retired*/ 0, /*xxh64 LDS depth (2/3/4/5 -> 1/2/4/3)*/ 0,
                                           /*zero copy*/ 1, /*xxh3 run-time size: 4-block batches*/ 1,
@@ -1475,7 +1475,8 @@ std::atomic<int64_t> g_tune[kTuneKeys] = {0, /*xxh3 blocks/CU*/ 0, /*xxh64 block
                                           /*retired (round 5 lab: service polls in flight)*/ 0,
                                           /*test only: service kernels serve nothing and leave this many us late*/ 0,
                                           /*zero-copy batches completing from their verdicts: event behind the kernel*/ 0,
-                                          /*sync host calls: microseconds of spinning before sleeping between checks (0 = spin)*/ 0};
+                                          /*sync host calls: microseconds of spinning before sleeping between checks (0 = spin)*/ 0,
+                                          /*validate service: polls read the kernel's departure words*/ 1};
 }
 int set_tuning(int key, int64_t value) {
     if (key <= 0 || key >= kTuneKeys || kRetired[key] || value < 0) return -1;
@@ -1982,6 +1983,15 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (__builtin_amdgcn_s_memrealtime() - t0 < exit_ticks) __builtin_amdgcn_s_sleep(127);
             }
+            // Departure: each wave's verdict and header stores complete at
+            // system scope, then one word says this workgroup has gone, so a
+            // host that sees it may re-arm the line (no store of this
+            // generation can land in it any more).
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(&box->departed[blockIdx.x], (uint32_t)gen, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         last = s_line[0];
@@ -2014,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_service(ServiceBox* box, int wpl, uint6
 
 hipError_t run_service(ServiceBox* d_box, int lines, int wpl, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                        uint64_t exit_ticks, hipStream_t s) {
-    if (lines < 1 || lines > kServiceMaxLines || wpl < 1 || lines * wpl > 256) return hipErrorInvalidValue;
+    if (lines < 1 || lines > kServiceMaxLines || wpl < 1 || lines * wpl > kServiceMaxWorkgroups) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_service, dim3((unsigned)(lines * wpl)), dim3(kBlock), 0, s, d_box, wpl, (uint64_t)gen,
                        idle_ticks, life_ticks, exit_ticks);
     return hipGetLastError();

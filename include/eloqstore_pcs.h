@@ -93,7 +93,7 @@ enum pcs_flags {
  *      PCS_COUNTER_SERVICE_REPOSTS (additive: no prototype changed)
  *   6  round 6: pcs_last_path / pcs_batch_path and the PCS_PATH_* bits,
  *      PCS_TUNE_SERVICE_SLOW_EXIT_TEST, PCS_TUNE_ZC_BATCH_EVENT, PCS_TUNE_SYNC_SPIN_US,
- *      pcs_thread_prepare (additive);
+ *      PCS_TUNE_SERVICE_DEPARTURE, pcs_thread_prepare (additive);
  *      pcs_stream_read_dev writes
  *      one word per 4 KiB (was per 64 KiB: size d_out for the new count) */
 #define PCS_ABI_VERSION 6
@@ -385,6 +385,14 @@ int pcs_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *
  *                                     throughout (lowest latency; a loaded
  *                                     store's sync callers then burn their
  *                                     cores)
+ *   PCS_TUNE_SERVICE_DEPARTURE    [1] a service kernel's workgroups store
+ *                                     their generation into the mailbox as
+ *                                     they leave; 1: a waiting request learns
+ *                                     that its line's workgroups have gone
+ *                                     from those words (re-posting at once)
+ *                                     and asks the runtime about the kernel
+ *                                     every 1 ms; 0: asks the runtime every
+ *                                     50 µs (round 6 before this key)
  * Keys 4, 5, 10, 12, 14, 16-22, 25, 29 and 32 selected variants that measured slower or no
  * better (XXH64 quad nt loads, in-place stamp widths, descriptor tile sorts,
  * 4 KiB slices, wave-dealt pages and slice streams, pipelined split-page
@@ -415,6 +423,7 @@ enum pcs_tune_key {
     PCS_TUNE_SERVICE_SLOW_EXIT_TEST = 33,
     PCS_TUNE_ZC_BATCH_EVENT = 34,
     PCS_TUNE_SYNC_SPIN_US = 35,
+    PCS_TUNE_SERVICE_DEPARTURE = 36,
 };
 int pcs_set_tuning(int key, int64_t value);
 int64_t pcs_get_tuning(int key); /* -1 for an unknown key */

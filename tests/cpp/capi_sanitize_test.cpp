@@ -195,10 +195,11 @@ static void abi4_no_device() {
     CHECK(pcs_get_tuning(PCS_TUNE_FAIL_INJECT) == 0 && pcs_get_tuning(PCS_TUNE_SERVICE_TEAR_TEST) == 0);
     // ABI 5: the re-post drill knob and counter
     CHECK(PCS_ABI_VERSION >= 5 && pcs_get_tuning(PCS_TUNE_SERVICE_REPOST_TEST) == 0);
-    CHECK(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) == 0 && pcs_get_tuning(36) == -1);
+    CHECK(pcs_counter(PCS_COUNTER_SERVICE_REPOSTS) == 0 && pcs_get_tuning(37) == -1);
     // ABI 6: the slow-exit test knob, the path bits and the thread prepare
     CHECK(PCS_ABI_VERSION >= 6 && pcs_get_tuning(PCS_TUNE_SERVICE_SLOW_EXIT_TEST) == 0);
     CHECK(pcs_get_tuning(PCS_TUNE_ZC_BATCH_EVENT) == 0 && pcs_get_tuning(PCS_TUNE_SYNC_SPIN_US) == 0);
+    CHECK(pcs_get_tuning(PCS_TUNE_SERVICE_DEPARTURE) == 1);
     CHECK((pcs_last_path() & ~63) == 0 && pcs_batch_path(nullptr) == 0);
     CHECK(pcs_thread_prepare() == PCS_ERR_NO_DEVICE);
     CHECK(pcs_get_tuning(32) == -1 && pcs_set_tuning(32, 2) == PCS_ERR_INVALID);  // retired (round 5)

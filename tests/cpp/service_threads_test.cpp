@@ -41,6 +41,8 @@
 // the path mix, restarts and latency percentiles -- overall and per op x
 // path (pcs_last_path / pcs_batch_path) x whether a restart was in flight,
 // plus the slowest requests with their attribution -- then "service soak ok".
+// PCS_DEPARTURE=0 (any mode) turns the kernels' departure words off: waiting
+// requests then learn that a kernel left from the runtime alone (every 50 us).
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -741,6 +743,8 @@ int main(int argc, char** argv) {
     oracle_fill_pages(pool, P, np, 0x7E57, 0);
     for (size_t i = 0; i < np; ++i) oracle_set_checksum(pool + i * P, P);
     eloqstore::RegisterPagePool(pool, np * P);
+    // PCS_DEPARTURE=0: the service's departure words off (every mode)
+    if (const char* d = std::getenv("PCS_DEPARTURE")) CHECK(pcs_set_tuning(PCS_TUNE_SERVICE_DEPARTURE, std::atoi(d)) == PCS_OK);
     // --slow-stop / --slow-timeout [RUNS]: RUNS runs (default 1) in this process
     if ((argc == 2 || argc == 3) &&
         (std::strcmp(argv[1], "--slow-stop") == 0 || std::strcmp(argv[1], "--slow-timeout") == 0)) {

@@ -377,6 +377,22 @@ def test_service_soak_under_restarts():
     print(r.stdout)
 
 
+@pytest.mark.parametrize("departure", ["0", "1"])
+def test_service_soak_departure_modes(departure):
+    """The soak (6 s) with the kernels' departure words off and on
+    (PCS_TUNE_SERVICE_DEPARTURE): waiting requests learn that their line's
+    workgroups left from the runtime every 50 us, or from the words the
+    workgroups store as they leave (the runtime then every 1 ms).  Restarts,
+    gate flips, torn-line and re-post drills: every result exact either way."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "service_threads_test")
+    env = dict(os.environ, PCS_DEPARTURE=departure)
+    r = subprocess.run([exe, "--soak", "6"], capture_output=True, text=True, timeout=100, env=env)
+    assert r.returncode == 0 and "service soak ok" in r.stdout, r.stdout + r.stderr
+    print(r.stdout)
+
+
 def test_stamp_done_bytes_under_threads():
     """The launch path alone (no service): eight native threads stamping
     small batches of their own zeroed pages, synchronously and through

@@ -254,17 +254,29 @@ int main(int argc, char** argv) {
                     "in_call/GiB", "saved/GiB", "served", "bad");
         double ref_per_gib = 0;
         for (int T : {1, 8}) {
-            for (const char* form : {"ref", "sync", "sync_sleep", "service", "async", "async_event", "async_service",
-                                     "async_service_q1"}) {
-                const bool svc = std::strstr(form, "service") != nullptr;
-                const bool ev = std::strcmp(form, "async_event") == 0;
+            for (const char* form : {"ref", "sync", "sync_sleep", "service", "service_d0", "async", "async_event",
+                                     "async_service", "async_service_d0", "async_service_q1", "async_service_q1_d0"}) {
+                // CPU_COST_FORMS: a comma-separated subset to run (all by default)
+                if (const char* only = std::getenv("CPU_COST_FORMS")) {
+                    const std::string list = std::string(",") + only + ",";
+                    if (list.find(std::string(",") + form + ",") == std::string::npos) continue;
+                }
+                // "_d0": the same form with the service's departure words off
+                // (PCS_TUNE_SERVICE_DEPARTURE = 0: the runtime is asked every 50 us)
+                std::string base = form;
+                const bool d0 = base.size() > 3 && base.compare(base.size() - 3, 3, "_d0") == 0;
+                if (d0) base.resize(base.size() - 3);
+                const bool svc = base.find("service") != std::string::npos;
+                const bool ev = base == "async_event";
                 pcs_set_tuning(PCS_TUNE_ZC_BATCH_EVENT, ev ? 1 : 0);
-                pcs_set_tuning(PCS_TUNE_SYNC_SPIN_US, std::strcmp(form, "sync_sleep") == 0 ? 30 : 0);
-                const int Q = std::strcmp(form, "async_service_q1") == 0 ? 1 : 4;
+                pcs_set_tuning(PCS_TUNE_SYNC_SPIN_US, base == "sync_sleep" ? 30 : 0);
+                pcs_set_tuning(PCS_TUNE_SERVICE_DEPARTURE, d0 ? 0 : 1);
+                const int Q = base == "async_service_q1" ? 1 : 4;
                 // a line per request that can be in flight (at most 8 lines)
-                if (svc) StartChecksumService(std::strcmp(form, "service") == 0 ? 4 : 2, 1000,
-                                              std::min(8, std::strcmp(form, "service") == 0 ? T : T * Q));
-                Point pt = run(pool, form, T, Q, write, secs, work_unit);
+                static const int max_lines = std::getenv("CPU_COST_MAX_LINES") ? std::atoi(std::getenv("CPU_COST_MAX_LINES")) : 8;
+                if (svc) StartChecksumService(base == "service" ? 4 : 2, 1000, std::min(max_lines, base == "service" ? T : T * Q));
+                Point pt = run(pool, base.c_str(), T, Q, write, secs, work_unit);
+                pt.form = form;
                 if (svc) StopChecksumService();
                 pt.path = svc ? "service" : std::strcmp(form, "ref") == 0 ? "cpu" : "zero-copy launch";
                 if (pt.form == "ref" && T == 1) ref_per_gib = pt.cpu_per_gib();
